@@ -1,0 +1,236 @@
+// stl_verify_core.h -- one Ed25519 verification per lane, with the exact
+// accept predicate of stellard's RippleAddress::verifySignature
+// (src/ripple_data/protocol/RippleAddress.cpp:190-200):
+//     crypto_sign_verify_detached(sig, hash, 32, pk) == 0   &&   S < L
+// where crypto_sign_verify_detached is libsodium's (not vendored; 1.0.18 is
+// the executable oracle here, 1.0.0 is what the reference pins):
+//   1.0.18: S < L, R not small order, A canonical, A not small order,
+//   both:   A decompresses, k = SHA-512(R||A||M) mod L,
+//           accept iff encode([k](-A) + [S]B) == R byte-for-byte (cofactorless)
+//   1.0.0:  (sig[63] & 0xE0) == 0 instead of the four 1.0.18 pre-checks.
+//
+// Scalar multiplication: joint fixed-window (signed radix 16) Straus with
+// shared doublings -- uniform control flow across the wave (no per-lane
+// sliding-window branches).  [k](-A) uses a 9-entry per-lane table of cached
+// multiples of -A held in a lane-interleaved HBM/L2 workspace; [S]B uses the
+// constant affine table of j*B.  The result is the same group element as
+// libsodium's sliding-window ge25519_double_scalarmult_vartime, so encode()
+// matches byte-for-byte.
+#pragma once
+#include "stl_ge25519.h"
+#include "stl_sc25519.h"
+#include "stl_sha512.h"
+
+namespace stl {
+
+enum : uint32_t {
+  kPolicySodium1018 = 0u,
+  kPolicyStellard100 = 1u,
+};
+
+STL_HD uint32_t small_order_word(int e, int i) {
+  const uint32_t bl[7][8] = {
+      {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+      {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+      {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
+      {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
+      {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+      {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+      {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu}};
+  return bl[e][i];
+}
+
+// ge25519_has_small_order: bytes 0..30 and (byte 31 & 0x7f) vs the 7 encodings
+STL_HD bool has_small_order(const uint32_t s[8]) {
+  bool any = false;
+#pragma unroll
+  for (int e = 0; e < 7; ++e) {
+    bool eq = (s[7] & 0x7fffffffu) == small_order_word(e, 7);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) eq = eq && s[i] == small_order_word(e, i);
+    any = any || eq;
+  }
+  return any;
+}
+
+// ge25519_is_canonical: the 255-bit y is < p
+STL_HD bool point_is_canonical(const uint32_t s[8]) {
+  bool top = (s[7] & 0x7fffffffu) == 0x7fffffffu;
+#pragma unroll
+  for (int i = 1; i < 7; ++i) top = top && s[i] == 0xffffffffu;
+  return !(top && s[0] >= 0xffffffedu);
+}
+
+// Pre-checks of crypto_sign_verify_detached for the selected policy.
+STL_HD bool verify_prechecks(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], uint32_t policy) {
+  if (policy == kPolicyStellard100) return (S[7] >> 29) == 0;  // sig[63] & 224
+  return sc_lt_L(S) && !has_small_order(R) && point_is_canonical(A) && !has_small_order(A);
+}
+
+// Per-lane table of cached multiples e*(-A), e = 0..8, 9 x uint4 per entry.
+// LaneStride = distance (in uint4) between consecutive lanes' copies of the
+// same (entry, quad): 64 on the device (one wave's lanes interleaved), 1 for
+// the host test harness.
+struct TableView {
+  uint4* base;
+  int stride;
+  STL_HD void store(int e, const ge_cached& c) const {
+    const uint32_t* w = &c.YpX.v[0];
+    uint32_t buf[36];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      buf[i] = c.YpX.v[i];
+      buf[9 + i] = c.YmX.v[i];
+      buf[18 + i] = c.Z.v[i];
+      buf[27 + i] = c.T2d.v[i];
+    }
+    (void)w;
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+      base[(e * 9 + q) * stride] = make_uint4(buf[4 * q], buf[4 * q + 1], buf[4 * q + 2], buf[4 * q + 3]);
+  }
+  STL_HD void load(int e, ge_cached& c) const {
+    uint32_t buf[36];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const uint4 v = base[(e * 9 + q) * stride];
+      buf[4 * q] = v.x;
+      buf[4 * q + 1] = v.y;
+      buf[4 * q + 2] = v.z;
+      buf[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      c.YpX.v[i] = buf[i];
+      c.YmX.v[i] = buf[9 + i];
+      c.Z.v[i] = buf[18 + i];
+      c.T2d.v[i] = buf[27 + i];
+    }
+  }
+};
+
+STL_HD void load_base_niels(ge_niels& n, const uint32_t (*tab)[27], int absd) {
+  const int idx = absd > 0 ? absd - 1 : 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    n.ypx.v[i] = tab[idx][i];
+    n.ymx.v[i] = tab[idx][9 + i];
+    n.xy2d.v[i] = tab[idx][18 + i];
+  }
+  // digit 0: the identity (1, 1, 0)
+  ge_niels id;
+  fe_1(id.ypx);
+  fe_1(id.ymx);
+  fe_0(id.xy2d);
+  const bool z = absd == 0;
+  fe_cmov(n.ypx, n.ypx, id.ypx, z);
+  fe_cmov(n.ymx, n.ymx, id.ymx, z);
+  fe_cmov(n.xy2d, n.xy2d, id.xy2d, z);
+}
+
+// R' = [k](-A) + [S]B  with k, S < 2^253.  negA is the decompressed -A.
+STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8], const uint32_t S[8],
+                              const TableView& tab, const uint32_t (*bniels)[27]) {
+  // ---- table of e*(-A), e = 0..8 ----
+  ge_cached c1, c;
+  ge_cached_0(c);
+  tab.store(0, c);
+  ge_p3_to_cached(c1, negA);
+  tab.store(1, c1);
+  ge_p1p1 t;
+  ge_p2 p2;
+  ge_p3 p3;
+  ge_p3_to_p2(p2, negA);
+  ge_p2_dbl(t, p2);
+  ge_p1p1_to_p3(p3, t);
+  ge_p3_to_cached(c, p3);
+  tab.store(2, c);
+  for (int e = 3; e <= 8; ++e) {
+    ge_add_cached(t, p3, c1);
+    ge_p1p1_to_p3(p3, t);
+    ge_p3_to_cached(c, p3);
+    tab.store(e, c);
+  }
+  // ---- signed radix-16 digits ----
+  uint32_t kd[8], sd[8];
+  sc_recode16(kd, k);
+  sc_recode16(sd, S);
+  // ---- main loop: 64 digit positions, most significant first ----
+  ge_p3 acc;
+  ge_p3_0(acc);
+  ge_p2 acc2;
+  uint32_t wa = 0, wb = 0;
+  for (int i = 63; i >= 0; --i) {
+    if ((i & 7) == 7) {
+      // fetch the next packed word (digits 8m..8m+7) by shifting the word array
+      wa = kd[7];
+      wb = sd[7];
+#pragma unroll
+      for (int m = 7; m > 0; --m) {
+        kd[m] = kd[m - 1];
+        sd[m] = sd[m - 1];
+      }
+    }
+    if (i != 63) {
+#pragma unroll 1
+      for (int r = 0; r < 3; ++r) {
+        ge_p2_dbl(t, acc2);
+        ge_p1p1_to_p2(acc2, t);
+      }
+      ge_p2_dbl(t, acc2);
+      ge_p1p1_to_p3(acc, t);
+    }
+    const int da = (int32_t)wa >> 28;
+    const int db = (int32_t)wb >> 28;
+    wa <<= 4;
+    wb <<= 4;
+    // A digit
+    const int ada = da < 0 ? -da : da;
+    tab.load(ada > 8 ? 8 : ada, c);
+    ge_cached_cneg(c, da < 0);
+    ge_add_cached(t, acc, c);
+    ge_p1p1_to_p3(acc, t);
+    // B digit
+    const int adb = db < 0 ? -db : db;
+    ge_niels n;
+    load_base_niels(n, bniels, adb > 8 ? 8 : adb);
+    ge_niels_cneg(n, db < 0);
+    ge_madd(t, acc, n);
+    ge_p1p1_to_p2(acc2, t);
+  }
+  out = acc2;
+}
+
+// Full check for one signature given k = H(R||A||M) mod L (8 words).
+STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
+                          uint32_t policy, const TableView& tab, const uint32_t (*bniels)[27]) {
+  bool ok = verify_prechecks(R, S, A, policy);
+  ge_p3 negA;
+  ok = ge_frombytes_negate_vartime(negA, A) && ok;
+  // S < 2^253 is guaranteed for accepted lanes under both policies; mask so a
+  // rejected lane still runs the same bounded digit range.
+  uint32_t Sm[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) Sm[i] = S[i];
+  Sm[7] &= 0x1fffffffu;
+  ge_p2 Rp;
+  double_scalarmult(Rp, negA, k, Sm, tab, bniels);
+  uint32_t enc[8];
+  ge_tobytes(enc, Rp);
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq = eq && enc[i] == R[i];
+  // stellard composite: && signatureIsCanonical (S < L)
+  return ok && eq && sc_lt_L(S);
+}
+
+// Fixed 32-byte message (the stellard signing hash): k computed in-lane.
+STL_HD bool verify_msg32(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t M[8],
+                         uint32_t policy, const TableView& tab, const uint32_t (*bniels)[27]) {
+  uint32_t h[16], k[8];
+  sha512_hram32(h, R, A, M);
+  sc_reduce64(k, h);
+  return verify_with_k(R, S, A, k, policy, tab, bniels);
+}
+
+}  // namespace stl

@@ -1,0 +1,94 @@
+// hostemu.cpp -- TEST HARNESS ONLY.  Compiles the device verify code
+// (stellard_amd/csrc/stl_verify_core.h, the exact functions the gfx950 kernel
+// runs) for the host so its logic and limb-bound discipline can be checked
+// against the oracle in the CPU test suite.  Not part of the product library
+// (libstl exposes no CPU verify path).
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+static std::atomic<uint64_t> g_bound_viol{0};
+static std::atomic<uint64_t> g_bound_checks{0};
+
+#define STL_BOUND_MUL(a, b) hostemu_check_mul((a), (b))
+#define STL_BOUND_SUB(a, b) hostemu_check_sub((a), (b))
+namespace stl { struct fe; }
+static void hostemu_check_mul(const stl::fe& a, const stl::fe& b);
+static void hostemu_check_sub(const stl::fe& a, const stl::fe& b);
+
+#include "../../stellard_amd/csrc/stl_base_table.h"
+#include "../../stellard_amd/csrc/stl_verify_core.h"
+
+static double alpha(const stl::fe& a) {
+  uint32_t m = 0;
+  for (int i = 0; i < 9; ++i) m = a.v[i] > m ? a.v[i] : m;
+  return m / 536870912.0;
+}
+static void hostemu_check_mul(const stl::fe& a, const stl::fe& b) {
+  g_bound_checks++;
+  if (alpha(a) * alpha(b) > 7.0) g_bound_viol++;
+}
+static void hostemu_check_sub(const stl::fe& a, const stl::fe& b) {
+  g_bound_checks++;
+  if (alpha(a) > 3.9 || alpha(b) > 3.9) g_bound_viol++;
+}
+
+static void load8(uint32_t w[8], const uint8_t* p) { std::memcpy(w, p, 32); }
+
+extern "C" {
+
+// Bitmap out, LSB-first; returns number of bound violations observed.
+uint64_t hostemu_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
+                              uint8_t* bitmap, uint32_t policy) {
+  std::vector<uint4> table(81);
+  stl::TableView tv{table.data(), 1};
+  std::memset(bitmap, 0, (n + 7) / 8);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t R[8], S[8], A[8], M[8];
+    load8(R, sig + 64 * i);
+    load8(S, sig + 64 * i + 32);
+    load8(A, pk + 32 * i);
+    load8(M, msg + 32 * i);
+    if (stl::verify_msg32(R, S, A, M, policy, tv, stl::kBaseNielsHost)) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  return g_bound_viol.load();
+}
+
+uint64_t hostemu_bound_checks(void) { return g_bound_checks.load(); }
+
+void hostemu_sha512_hram32(const uint8_t* R, const uint8_t* A, const uint8_t* M, uint8_t out[64]) {
+  uint32_t r[8], a[8], m[8], h[16];
+  load8(r, R); load8(a, A); load8(m, M);
+  stl::sha512_hram32(h, r, a, m);
+  std::memcpy(out, h, 64);
+}
+
+void hostemu_sc_reduce64(const uint8_t in[64], uint8_t out[32]) {
+  uint32_t x[16], o[8];
+  std::memcpy(x, in, 64);
+  stl::sc_reduce64(o, x);
+  std::memcpy(out, o, 32);
+}
+
+void hostemu_fe_mul_bytes(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  uint32_t wa[8], wb[8], wo[8];
+  load8(wa, a); load8(wb, b);
+  stl::fe fa, fb, fo;
+  stl::fe_frombytes(fa, wa);
+  stl::fe_frombytes(fb, wb);
+  stl::fe_mul(fo, fa, fb);
+  stl::fe_tobytes(wo, fo);
+  std::memcpy(out, wo, 32);
+}
+
+void hostemu_fe_invert_bytes(const uint8_t a[32], uint8_t out[32]) {
+  uint32_t wa[8], wo[8];
+  load8(wa, a);
+  stl::fe fa, fo;
+  stl::fe_frombytes(fa, wa);
+  stl::fe_invert(fo, fa);
+  stl::fe_tobytes(wo, fo);
+  std::memcpy(out, wo, 32);
+}
+}
