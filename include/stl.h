@@ -1,0 +1,119 @@
+/*
+ * stl.h -- C ABI of libstl, the MI355X (gfx950) batched Ed25519
+ * transaction-signature verifier for stellard.
+ *
+ * Drop-in boundary (reference = hfeeki/stellard, libsodium not vendored):
+ *
+ *   lower boundary replaced: libsodium
+ *     int crypto_sign_verify_detached(const unsigned char *sig,
+ *                                     const unsigned char *m,
+ *                                     unsigned long long mlen,
+ *                                     const unsigned char *pk);
+ *     called at src/ripple_data/protocol/RippleAddress.cpp:196-197 and
+ *     src/ripple_data/crypto/StellarPublicKey.cpp:73-74
+ *   upper boundary mirrored:
+ *     bool RippleAddress::verifySignature(uint256 const&, Blob const&) const
+ *       src/ripple_data/protocol/RippleAddress.cpp:190-200 (= verify && S<L)
+ *     bool SerializedTransaction::checkSign(const RippleAddress&) const
+ *       src/ripple_app/misc/SerializedTransaction.cpp:220-230
+ *       (= SHA512Half(signing preimage) then verifySignature)
+ *
+ * Conventions: plain pointers and sizes, caller-owned host buffers, no
+ * exceptions across the ABI, nothing retained after return.  Accept bitmaps
+ * are ceil(n/8) bytes, bit i = byte i>>3, bit (i & 7), LSB first; a set bit
+ * means ACCEPT under stellard's composite predicate (verify && S < L).
+ *
+ * Return codes: STL_OK (0) or a negative error.  On error the bitmap is
+ * undefined and the caller MUST fall back to its own per-signature check --
+ * a device error is never reported as a reject.  libstl itself has no CPU
+ * verify path.
+ */
+#ifndef STL_H
+#define STL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STL_ABI_VERSION 1
+
+/* ---- return codes ---- */
+#define STL_OK 0
+#define STL_EINVAL (-22)   /* bad argument (null pointer with n > 0, bad flags, bad length) */
+#define STL_ENODEV (-19)   /* no gfx950 device available / not initialised */
+#define STL_ENOMEM (-12)   /* device or host allocation failed */
+#define STL_EHIP (-1000)   /* HIP runtime error (kernel launch, copy, sync) */
+
+/* ---- flags ---- */
+/* Accept predicate of crypto_sign_verify_detached to reproduce.  Default is
+ * the container's executable oracle, libsodium 1.0.18 (S < L, R and A not of
+ * small order, A canonical).  STELLARD_1_0_0 reproduces the ref10-era
+ * predicate of the libsodium the reference pins (Dockerfile:9-10): only
+ * (sig[63] & 0xE0) == 0; parity for it is unpinned offline. */
+#define STL_POLICY_SODIUM_1_0_18 0x0u
+#define STL_POLICY_STELLARD_1_0_0 0x1u
+#define STL_POLICY_MASK 0x1u
+/* stellard's crypto_sign_check_S_lt_l (RippleAddress.cpp:226-252) is always
+ * applied (composite predicate); the flag exists for ABI symmetry. */
+#define STL_REQUIRE_S_LT_L 0x2u
+
+typedef struct stl_config {
+  uint32_t struct_size;  /* sizeof(stl_config) */
+  int32_t device_count;  /* devices to use; <= 0 = all visible */
+  int32_t first_device;  /* first HIP ordinal to use */
+  uint32_t flags;        /* reserved, 0 */
+} stl_config;
+
+/* Replaces/augments sodium_init() (src/ripple_app/ripple_app.cpp:129-132).
+ * Idempotent; cfg may be NULL (all devices).  Thread-safe. */
+int stl_init(const stl_config *cfg);
+void stl_shutdown(void);
+int stl_device_count(void);
+const char *stl_version(void);
+const char *stl_strerror(int rc);
+
+/* Same signature and return convention as libsodium's
+ * crypto_sign_verify_detached (0 = accept, -1 = reject), plus stellard's S<L:
+ * i.e. exactly RippleAddress::verifySignature's bool as 0/-1.  Runs on the GPU
+ * (batch of one); returns a value < -1 on a device error. */
+int stl_ed25519_verify_detached(const uint8_t *sig, const uint8_t *m, unsigned long long mlen,
+                                const uint8_t *pk);
+
+/* n signatures over 32-byte messages (the stellard signing hash).
+ * sig: n*64 bytes (R || S), msg: n*32, pk: n*32 -- caller host memory.
+ * Sharded by index over the initialised devices (contiguous, 64-aligned). */
+int stl_ed25519_verify_batch(const uint8_t *sig, const uint8_t *msg, const uint8_t *pk, size_t n,
+                             uint8_t *accept_bitmap, uint32_t flags);
+
+/* checkSign equivalent: msg_i = SHA512Half(preimage_i), then verify.
+ * preimage_i = preimages[offset[i] .. offset[i]+len[i]) and already includes
+ * the 4-byte "STX\0" prefix (HashPrefix::txSign, HashPrefix.cpp:30). */
+int stl_tx_verify_batch(const uint8_t *preimages, const uint64_t *offset, const uint32_t *len,
+                        const uint8_t *sig, const uint8_t *pk, size_t n, uint8_t *accept_bitmap,
+                        uint32_t flags);
+
+/* ---- device-resident entry points (asynchronous on the caller's stream) ----
+ * All pointers are device pointers on the current HIP device; stream is a
+ * hipStream_t (NULL = default stream).  The bitmap is written as
+ * ceil(n/64) little-endian 64-bit words (same bit order as above). */
+int stl_ed25519_verify_batch_device(const uint8_t *d_sig, const uint8_t *d_msg, const uint8_t *d_pk,
+                                    size_t n, uint64_t *d_bitmap_words, uint32_t flags, void *stream);
+
+/* SHA512Half over n preimages -> d_msg (n*32 bytes). */
+int stl_tx_hash_batch_device(const uint8_t *d_preimages, const uint64_t *d_offset, const uint32_t *d_len,
+                             size_t n, uint8_t *d_msg, void *stream);
+
+/* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;
+ * EdKeyPair::setSeed, EdKeyPair.cpp:25-33): RFC 8032 keypair from a 32-byte
+ * seed and a detached signature over a 32-byte message. */
+int stl_ed25519_sign_batch_device(const uint8_t *d_seed, const uint8_t *d_msg, size_t n, uint8_t *d_pk,
+                                  uint8_t *d_sig, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STL_H */

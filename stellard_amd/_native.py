@@ -1,0 +1,81 @@
+"""ctypes binding of libstl.so (the C ABI in include/stl.h).
+
+The shared library is built in-tree by ``stellard_amd.build`` (hipcc,
+--offload-arch=gfx950).  There is no Python or CPU fallback: if the library is
+missing this module raises, so a GPU run can never silently verify on the host.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstl.so")
+
+STL_OK = 0
+STL_EINVAL = -22
+STL_ENODEV = -19
+STL_ENOMEM = -12
+STL_EHIP = -1000
+
+STL_POLICY_SODIUM_1_0_18 = 0x0
+STL_POLICY_STELLARD_1_0_0 = 0x1
+STL_POLICY_MASK = 0x1
+STL_REQUIRE_S_LT_L = 0x2
+
+# Every entry point include/stl.h declares: (name, restype, argtypes)
+_P = ctypes.c_void_p
+_U8P = ctypes.c_void_p
+SYMBOLS = [
+    ("stl_init", ctypes.c_int, [_P]),
+    ("stl_shutdown", None, []),
+    ("stl_device_count", ctypes.c_int, []),
+    ("stl_version", ctypes.c_char_p, []),
+    ("stl_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("stl_ed25519_verify_detached", ctypes.c_int, [_U8P, _U8P, ctypes.c_ulonglong, _U8P]),
+    ("stl_ed25519_verify_batch", ctypes.c_int, [_U8P, _U8P, _U8P, ctypes.c_size_t, _U8P, ctypes.c_uint32]),
+    ("stl_tx_verify_batch", ctypes.c_int,
+     [_U8P, _P, _P, _U8P, _U8P, ctypes.c_size_t, _U8P, ctypes.c_uint32]),
+    ("stl_ed25519_verify_batch_device", ctypes.c_int,
+     [_U8P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
+    ("stl_tx_hash_batch_device", ctypes.c_int, [_U8P, _P, _P, ctypes.c_size_t, _U8P, _P]),
+    ("stl_ed25519_sign_batch_device", ctypes.c_int, [_U8P, _U8P, ctypes.c_size_t, _U8P, _U8P, _P]),
+]
+
+
+class StlError(RuntimeError):
+    def __init__(self, rc, what=""):
+        self.rc = rc
+        super().__init__(f"libstl error {rc} ({strerror(rc)}) {what}".strip())
+
+
+_lib = None
+
+
+def load():
+    """Load libstl.so and bind every exported symbol; raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(libstl has no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SYMBOLS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def strerror(rc):
+    try:
+        return load().stl_strerror(rc).decode()
+    except Exception:  # noqa: BLE001 - used while formatting an error
+        return "?"
+
+
+def check(rc, what=""):
+    if rc != STL_OK:
+        raise StlError(rc, what)
+    return rc

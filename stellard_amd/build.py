@@ -1,0 +1,75 @@
+"""In-tree build of every native artefact (no cmake, no JIT cache):
+
+  stellard_amd/libstl.so         product: gfx950 kernels + C ABI (hipcc)
+  tests/native/libhostemu.so     test harness: the device verify code compiled
+                                 for the host (bound checks on)
+  oracle/build/liboracle.so      test oracle: CPU restatement (make)
+  oracle/_ref/libsodium_ref.so   test oracle: reference call path over libsodium
+
+Usage: python -m stellard_amd.build [--product-only]
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "stellard_amd", "csrc")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+PRODUCT_SRCS = ["stl_kernels.hip", "stl_api.cpp"]
+PRODUCT_DEPS = PRODUCT_SRCS + ["stl_kernels.h", "stl_verify_core.h", "stl_fe25519.h", "stl_ge25519.h",
+                               "stl_sc25519.h", "stl_sha512.h", "stl_base_table.h",
+                               os.path.join("..", "..", "include", "stl.h")]
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, cwd=ROOT):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, cwd=cwd, check=True)
+
+
+def build_product(force=False, extra_flags=()):
+    out = os.path.join(ROOT, "stellard_amd", "libstl.so")
+    deps = [os.path.join(CSRC, d) for d in PRODUCT_DEPS]
+    if force or extra_flags or _stale(out, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *extra_flags,
+              "-o", out] + [os.path.join(CSRC, s) for s in PRODUCT_SRCS])
+    return out
+
+
+def build_hostemu(force=False):
+    out = os.path.join(ROOT, "tests", "native", "libhostemu.so")
+    src = os.path.join(ROOT, "tests", "native", "hostemu.cpp")
+    deps = [src] + [os.path.join(CSRC, d) for d in PRODUCT_DEPS]
+    if force or _stale(out, deps):
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", "-o", out, src])
+    return out
+
+
+def build_oracle():
+    oracle = os.path.join(ROOT, "oracle")
+    targets = ["build/liboracle.so"]
+    # the libsodium harness only builds where libsodium's headers exist
+    if os.path.exists("/opt/conda/include/sodium.h"):
+        targets.append("_ref/libsodium_ref.so")
+    _run(["make", "-s", "-C", oracle] + targets)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    build_product(force="--force" in argv)
+    if "--product-only" not in argv:
+        build_hostemu(force="--force" in argv)
+        build_oracle()
+
+
+if __name__ == "__main__":
+    main()

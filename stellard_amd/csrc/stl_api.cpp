@@ -1,0 +1,355 @@
+// stl_api.cpp -- host side of libstl: the extern "C" boundary declared in
+// include/stl.h.  Owns devices, streams, workspaces and staging buffers; has
+// no CPU verification path (a device failure returns < 0 and the caller --
+// stellard -- falls back to libsodium, as SURVEY.md section 8b requires).
+//
+// Threading: stellard calls verify concurrently from JobQueue workers
+// (JobQueue.cpp:217-243).  Every device has a mutex that serialises the host
+// batch entry points on that device; the device-resident entry points key
+// their workspace by (device, stream) so concurrent streams never share one.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/stl.h"
+#include "stl_kernels.h"
+
+namespace {
+
+#define STL_TRY(expr)                        \
+  do {                                       \
+    hipError_t e_ = (expr);                  \
+    if (e_ != hipSuccess) return STL_EHIP;   \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return STL_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) return STL_ENOMEM;
+    cap = bytes;
+    return STL_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Device {
+  int ordinal = 0;
+  int cus = 0;
+  uint32_t grid = 0;  // resident workgroups for the verify kernel
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf ws, sig, msg, pk, bitmap, pre, off, len;
+  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;  // device-resident API
+  std::mutex ws_mu;
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<Device>> g_devs;
+bool g_init = false;
+
+int current_device_index() {
+  int ord = -1;
+  if (hipGetDevice(&ord) != hipSuccess) return -1;
+  for (size_t i = 0; i < g_devs.size(); ++i)
+    if (g_devs[i]->ordinal == ord) return (int)i;
+  return -1;
+}
+
+int setup_device(Device& d) {
+  STL_TRY(hipSetDevice(d.ordinal));
+  hipDeviceProp_t prop;
+  STL_TRY(hipGetDeviceProperties(&prop, d.ordinal));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return STL_ENODEV;
+  d.cus = prop.multiProcessorCount;
+  int per_cu = 0;
+  STL_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stl::kernel_verify_msg32(), stl::kBlock, 0));
+  if (per_cu < 1) per_cu = 1;
+  d.grid = (uint32_t)(d.cus * per_cu);
+  STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  return STL_OK;
+}
+
+int ensure_init() {
+  if (g_init) return STL_OK;
+  return stl_init(nullptr);
+}
+
+// Workspace for (device, stream) pairs used by the device-resident API.
+int stream_workspace(Device& d, hipStream_t s, uint4** ws) {
+  std::lock_guard<std::mutex> lk(d.ws_mu);
+  auto& slot = d.stream_ws[s];
+  if (!slot) slot.reset(new DevBuf());
+  int rc = slot->ensure(stl::kWsBytesPerBlock * d.grid);
+  if (rc) return rc;
+  *ws = static_cast<uint4*>(slot->p);
+  return STL_OK;
+}
+
+uint32_t grid_for(const Device& d, size_t n) {
+  const size_t tiles = (n + stl::kBlock - 1) / stl::kBlock;
+  return (uint32_t)std::max<size_t>(1, std::min<size_t>(tiles, d.grid));
+}
+
+// Contiguous 64-aligned shard of [0, n) for device r of g.
+void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
+  const size_t words = (n + 63) / 64;
+  const size_t per = (words + g - 1) / g;
+  *lo = std::min(n, (size_t)r * per * 64);
+  *hi = std::min(n, (size_t)(r + 1) * per * 64);
+}
+
+// Verify one shard [lo, hi) on device d, synchronously; writes the host bitmap
+// bytes [lo/8, ceil(hi/8)).  msg32 == nullptr means tx mode (preimages).
+int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t* pk, const uint8_t* pre,
+              const uint64_t* off, const uint32_t* len, size_t lo, size_t hi, uint8_t* bitmap, uint32_t policy) {
+  const size_t n = hi - lo;
+  if (n == 0) return STL_OK;
+  std::lock_guard<std::mutex> lk(d.mu);
+  STL_TRY(hipSetDevice(d.ordinal));
+  int rc;
+  const size_t words = (n + 63) / 64;
+  if ((rc = d.ws.ensure(stl::kWsBytesPerBlock * d.grid)) || (rc = d.sig.ensure(n * 64)) ||
+      (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)))
+    return rc;
+  hipStream_t s = d.stream;
+  STL_TRY(hipMemcpyAsync(d.sig.p, sig + 64 * lo, n * 64, hipMemcpyHostToDevice, s));
+  STL_TRY(hipMemcpyAsync(d.pk.p, pk + 32 * lo, n * 32, hipMemcpyHostToDevice, s));
+  if (msg32) {
+    STL_TRY(hipMemcpyAsync(d.msg.p, msg32 + 32 * lo, n * 32, hipMemcpyHostToDevice, s));
+  } else {
+    // tx mode: copy this shard's preimage bytes with offsets rebased to 0
+    const uint64_t base = off[lo];
+    uint64_t end = base;
+    std::vector<uint64_t> roff(n);
+    for (size_t i = 0; i < n; ++i) {
+      if (off[lo + i] < base) return STL_EINVAL;
+      roff[i] = off[lo + i] - base;
+      end = std::max<uint64_t>(end, off[lo + i] + len[lo + i]);
+    }
+    const size_t bytes = (size_t)(end - base);
+    if ((rc = d.pre.ensure(bytes ? bytes : 1)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4))) return rc;
+    if (bytes) STL_TRY(hipMemcpyAsync(d.pre.p, pre + base, bytes, hipMemcpyHostToDevice, s));
+    STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, s));
+    STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, s));
+    STL_TRY(stl::launch_tx_hash(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p),
+                                static_cast<uint32_t*>(d.len.p), (uint32_t)n, static_cast<uint8_t*>(d.msg.p), s));
+  }
+  STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
+                             static_cast<uint8_t*>(d.pk.p), (uint32_t)n, static_cast<uint64_t*>(d.bitmap.p), policy,
+                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false, s));
+  std::vector<uint8_t> host_words(words * 8);
+  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
+  STL_TRY(hipStreamSynchronize(s));
+  // lo is a multiple of 64, so the shard starts on a byte boundary
+  std::memcpy(bitmap + lo / 8, host_words.data(), (n + 7) / 8);
+  return STL_OK;
+}
+
+int run_batch(const uint8_t* sig, const uint8_t* msg32, const uint8_t* pk, const uint8_t* pre, const uint64_t* off,
+              const uint32_t* len, size_t n, uint8_t* bitmap, uint32_t flags) {
+  if (n == 0) return STL_OK;
+  if (!sig || !pk || !bitmap || (!msg32 && (!pre || !off || !len))) return STL_EINVAL;
+  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L)) return STL_EINVAL;
+  int rc = ensure_init();
+  if (rc) return rc;
+  const uint32_t policy = flags & STL_POLICY_MASK;
+  const int g = (int)g_devs.size();
+  if (g == 0) return STL_ENODEV;
+  // one kernel launch handles up to 2^32-64 signatures per shard
+  const size_t kMaxShard = (size_t)1 << 31;
+  int gg = (int)std::max<size_t>((size_t)g, (n + kMaxShard - 1) / kMaxShard);
+  std::vector<int> rcs(gg, STL_OK);
+  std::vector<std::thread> th;
+  for (int r = 0; r < gg; ++r) {
+    size_t lo, hi;
+    shard(n, r, gg, &lo, &hi);
+    Device& d = *g_devs[r % g];
+    if (gg == 1) {
+      rcs[r] = run_shard(d, sig, msg32, pk, pre, off, len, lo, hi, bitmap, policy);
+    } else {
+      th.emplace_back([&, r, lo, hi]() { rcs[r] = run_shard(*g_devs[r % g], sig, msg32, pk, pre, off, len, lo, hi, bitmap, policy); });
+    }
+  }
+  for (auto& t : th) t.join();
+  for (int r : rcs)
+    if (r) return r;
+  return STL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int stl_init(const stl_config* cfg) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_init) return STL_OK;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return STL_ENODEV;
+  int first = 0, want = count;
+  if (cfg) {
+    if (cfg->struct_size != sizeof(stl_config)) return STL_EINVAL;
+    first = cfg->first_device;
+    if (cfg->device_count > 0) want = cfg->device_count;
+  }
+  if (const char* env = std::getenv("STL_DEVICES")) want = std::max(1, std::atoi(env));
+  if (first < 0 || first >= count) return STL_EINVAL;
+  want = std::min(want, count - first);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (int i = 0; i < want; ++i) {
+    std::unique_ptr<Device> d(new Device());
+    d->ordinal = first + i;
+    int rc = setup_device(*d);
+    if (rc) {
+      (void)hipSetDevice(prev);
+      g_devs.clear();
+      return rc;
+    }
+    g_devs.push_back(std::move(d));
+  }
+  (void)hipSetDevice(prev);
+  g_init = true;
+  return STL_OK;
+}
+
+void stl_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& d : g_devs) {
+    std::lock_guard<std::mutex> dl(d->mu);
+    (void)hipSetDevice(d->ordinal);
+    (void)hipStreamSynchronize(d->stream);
+    for (DevBuf* b : {&d->ws, &d->sig, &d->msg, &d->pk, &d->bitmap, &d->pre, &d->off, &d->len}) b->release();
+    for (auto& kv : d->stream_ws) kv.second->release();
+    (void)hipStreamDestroy(d->stream);
+  }
+  g_devs.clear();
+  g_init = false;
+}
+
+int stl_device_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return (int)g_devs.size();
+}
+
+const char* stl_version(void) { return "stl 0.1.0 (gfx950, abi 1)"; }
+
+const char* stl_strerror(int rc) {
+  switch (rc) {
+    case STL_OK: return "ok";
+    case STL_EINVAL: return "invalid argument";
+    case STL_ENODEV: return "no gfx950 device";
+    case STL_ENOMEM: return "out of memory";
+    case STL_EHIP: return "HIP runtime error";
+    default: return "unknown error";
+  }
+}
+
+int stl_ed25519_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
+                             uint8_t* accept_bitmap, uint32_t flags) {
+  if (n && !msg) return STL_EINVAL;
+  return run_batch(sig, msg, pk, nullptr, nullptr, nullptr, n, accept_bitmap, flags);
+}
+
+int stl_tx_verify_batch(const uint8_t* preimages, const uint64_t* offset, const uint32_t* len, const uint8_t* sig,
+                        const uint8_t* pk, size_t n, uint8_t* accept_bitmap, uint32_t flags) {
+  return run_batch(sig, nullptr, pk, preimages, offset, len, n, accept_bitmap, flags);
+}
+
+int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned long long mlen, const uint8_t* pk) {
+  if (!sig || !pk || (mlen && !m)) return STL_EINVAL;
+  if (mlen == 32) {
+    uint8_t bit = 0;
+    int rc = stl_ed25519_verify_batch(sig, m, pk, 1, &bit, STL_POLICY_SODIUM_1_0_18);
+    if (rc) return rc;
+    return (bit & 1) ? 0 : -1;
+  }
+  // arbitrary-length message: k = H(R||A||m) mod L on the device, then verify
+  int rc = ensure_init();
+  if (rc) return rc;
+  Device& d = *g_devs[0];
+  std::lock_guard<std::mutex> lk(d.mu);
+  STL_TRY(hipSetDevice(d.ordinal));
+  if ((rc = d.ws.ensure(stl::kWsBytesPerBlock * d.grid)) || (rc = d.sig.ensure(64)) || (rc = d.pk.ensure(32)) ||
+      (rc = d.msg.ensure(32)) || (rc = d.bitmap.ensure(8)) || (rc = d.pre.ensure(mlen ? mlen : 1)) ||
+      (rc = d.off.ensure(16)))
+    return rc;
+  hipStream_t s = d.stream;
+  const uint64_t hostmeta[2] = {0, mlen};
+  STL_TRY(hipMemcpyAsync(d.sig.p, sig, 64, hipMemcpyHostToDevice, s));
+  STL_TRY(hipMemcpyAsync(d.pk.p, pk, 32, hipMemcpyHostToDevice, s));
+  if (mlen) STL_TRY(hipMemcpyAsync(d.pre.p, m, mlen, hipMemcpyHostToDevice, s));
+  STL_TRY(hipMemcpyAsync(d.off.p, hostmeta, 16, hipMemcpyHostToDevice, s));
+  uint64_t* meta = static_cast<uint64_t*>(d.off.p);
+  STL_TRY(stl::launch_hram_var(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.pk.p),
+                               static_cast<uint8_t*>(d.pre.p), meta, meta + 1, 1, static_cast<uint8_t*>(d.msg.p), s));
+  STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
+                             static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
+                             STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true, s));
+  uint64_t word = 0;
+  STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
+  STL_TRY(hipStreamSynchronize(s));
+  return (word & 1) ? 0 : -1;
+}
+
+int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, const uint8_t* d_pk, size_t n,
+                                    uint64_t* d_bitmap_words, uint32_t flags, void* stream) {
+  if (n == 0) return STL_OK;
+  if (!d_sig || !d_msg || !d_pk || !d_bitmap_words) return STL_EINVAL;
+  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L)) return STL_EINVAL;
+  if (n > 0xffffffc0ull) return STL_EINVAL;
+  int rc = ensure_init();
+  if (rc) return rc;
+  const int di = current_device_index();
+  if (di < 0) return STL_ENODEV;
+  Device& d = *g_devs[di];
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint4* ws = nullptr;
+  if ((rc = stream_workspace(d, s, &ws))) return rc;
+  STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, flags & STL_POLICY_MASK, ws,
+                             grid_for(d, n), false, s));
+  return STL_OK;
+}
+
+int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offset, const uint32_t* d_len, size_t n,
+                             uint8_t* d_msg, void* stream) {
+  if (n == 0) return STL_OK;
+  if (!d_preimages || !d_offset || !d_len || !d_msg || n > 0xffffffc0ull) return STL_EINVAL;
+  int rc = ensure_init();
+  if (rc) return rc;
+  STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, static_cast<hipStream_t>(stream)));
+  return STL_OK;
+}
+
+int stl_ed25519_sign_batch_device(const uint8_t* d_seed, const uint8_t* d_msg, size_t n, uint8_t* d_pk,
+                                  uint8_t* d_sig, void* stream) {
+  if (n == 0) return STL_OK;
+  if (!d_seed || !d_msg || !d_pk || !d_sig || n > 0xffffffc0ull) return STL_EINVAL;
+  int rc = ensure_init();
+  if (rc) return rc;
+  const int di = current_device_index();
+  if (di < 0) return STL_ENODEV;
+  Device& d = *g_devs[di];
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint4* ws = nullptr;
+  if ((rc = stream_workspace(d, s, &ws))) return rc;
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, ws, grid_for(d, n), s));
+  return STL_OK;
+}
+
+}  // extern "C"

@@ -33,6 +33,15 @@
 #define STL_BOUND_SUB(a, b)
 #endif
 
+// Scheduling fence after each field multiply: keeps the pre-RA scheduler from
+// software-pipelining consecutive products (which multiplies live registers
+// and forced spills at 2-4 waves/SIMD).  Device-only hint; no-op on the host.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define STL_FE_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define STL_FE_FENCE()
+#endif
+
 namespace stl {
 
 constexpr uint32_t M29 = 0x1fffffffu;
@@ -93,72 +102,83 @@ STL_HD void fe_cmov(fe& h, const fe& a, const fe& b, bool c) {
   for (int i = 0; i < 9; ++i) h.v[i] = c ? b.v[i] : a.v[i];
 }
 
-// Reduce 17 column sums c[0..16] (each < 63 * 2^58) to 9 limbs.
-STL_HD void fe_reduce_cols(fe& h, uint64_t c[17]) {
-  uint64_t carry = 0;
+// Product-scanning reduction shared by fe_mul / fe_sq.  COL(k) yields the
+// 64-bit sum of the partial products of column k (k = 0..16, each
+// < 63 * 2^58).  The high columns 9..16 are produced first and normalised to
+// 29-bit digits on the fly; each then folds into column k-9 with weight
+// 2^261 == 64 * 19 = 1216 (mod p).  Only one 64-bit column accumulator is live
+// at a time (register pressure of the verify kernel).
+#define STL_FE_REDUCE_COLUMNS(h, COL)                                   \
+  do {                                                                  \
+    uint32_t hi_[8];                                                    \
+    uint64_t carry_ = 0;                                                \
+    _Pragma("unroll") for (int k = 9; k < 17; ++k) {                    \
+      const uint64_t t_ = COL(k) + carry_;                              \
+      hi_[k - 9] = (uint32_t)t_ & M29;                                  \
+      carry_ = t_ >> 29;                                                \
+    }                                                                   \
+    const uint64_t top_ = carry_; /* weight 2^(29*17) */                \
+    carry_ = 0;                                                         \
+    _Pragma("unroll") for (int k = 0; k < 9; ++k) {                     \
+      const uint64_t f_ = k < 8 ? (uint64_t)hi_[k < 8 ? k : 0] * 1216u  \
+                                : top_ * 1216u;                         \
+      const uint64_t t_ = COL(k) + f_ + carry_;                         \
+      (h).v[k] = (uint32_t)t_ & M29;                                    \
+      carry_ = t_ >> 29;                                                \
+    }                                                                   \
+    const uint64_t u_ = (uint64_t)(h).v[0] + carry_ * 1216u;            \
+    (h).v[0] = (uint32_t)u_ & M29;                                      \
+    (h).v[1] += (uint32_t)(u_ >> 29);                                   \
+  } while (0)
+
+STL_HD uint64_t fe_mul_col(const fe& a, const fe& b, int k) {
+  uint64_t acc = 0;
 #pragma unroll
-  for (int k = 9; k < 17; ++k) {
-    uint64_t t = c[k] + carry;
-    c[k] = t & M29;
-    carry = t >> 29;
+  for (int i = 0; i < 9; ++i) {
+    const int j = k - i;
+    if (j < 0 || j > 8) continue;
+    acc += (uint64_t)a.v[i] * b.v[j];
   }
-  // columns 9..16 and the carry out of column 16 have weight 2^(29k) =
-  // 2^(29(k-9)) * 2^261, and 2^261 == 64 * 19 = 1216 (mod p)
+  return acc;
+}
+
+// d = 2a (precomputed); column k of a^2 = sum_{i<j} d_i a_j + [k even] a_{k/2}^2
+STL_HD uint64_t fe_sq_col(const fe& a, const uint32_t d[9], int k) {
+  uint64_t acc = 0;
 #pragma unroll
-  for (int k = 9; k < 17; ++k) c[k - 9] += c[k] * 1216u;
-  c[8] += carry * 1216u;
-  carry = 0;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    uint64_t t = c[k] + carry;
-    h.v[k] = (uint32_t)t & M29;
-    carry = t >> 29;
+  for (int i = 0; i < 9; ++i) {
+    const int j = k - i;
+    if (j <= i || j > 8) continue;
+    acc += (uint64_t)d[i] * a.v[j];
   }
-  uint64_t t = (uint64_t)h.v[0] + carry * 1216u;
-  h.v[0] = (uint32_t)t & M29;
-  h.v[1] += (uint32_t)(t >> 29);
+  if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+  return acc;
 }
 
 STL_HD void fe_mul(fe& h, const fe& a, const fe& b) {
   STL_BOUND_MUL(a, b);
-  uint64_t c[17];
-#pragma unroll
-  for (int k = 0; k < 17; ++k) {
-    uint64_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int j = k - i;
-      if (j < 0 || j > 8) continue;
-      acc += (uint64_t)a.v[i] * b.v[j];
-    }
-    c[k] = acc;
-  }
-  fe_reduce_cols(h, c);
+  const fe a_ = a, b_ = b;  // h may alias a or b
+#define STL_MUL_COL(k) fe_mul_col(a_, b_, (k))
+  STL_FE_REDUCE_COLUMNS(h, STL_MUL_COL);
+#undef STL_MUL_COL
+  STL_FE_FENCE();
 }
 
 STL_HD void fe_sq(fe& h, const fe& a) {
   STL_BOUND_MUL(a, a);
+  const fe a_ = a;
   uint32_t d[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;  // alpha <= 2.64 => fits 32 bits
-  uint64_t c[17];
-#pragma unroll
-  for (int k = 0; k < 17; ++k) {
-    uint64_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int j = k - i;
-      if (j <= i || j > 8) continue;
-      acc += (uint64_t)d[i] * a.v[j];
-    }
-    if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
-    c[k] = acc;
-  }
-  fe_reduce_cols(h, c);
+  for (int i = 0; i < 9; ++i) d[i] = a_.v[i] << 1;  // alpha <= 2.64 => fits 32 bits
+#define STL_SQ_COL(k) fe_sq_col(a_, d, (k))
+  STL_FE_REDUCE_COLUMNS(h, STL_SQ_COL);
+#undef STL_SQ_COL
+  STL_FE_FENCE();
 }
 
 STL_HD void fe_sqn(fe& h, const fe& a, int n) {
   fe_sq(h, a);
+#pragma unroll 1
   for (int i = 1; i < n; ++i) fe_sq(h, h);
 }
 

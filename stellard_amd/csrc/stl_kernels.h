@@ -1,0 +1,25 @@
+// stl_kernels.h -- launch interface between stl_api.cpp (host) and
+// stl_kernels.hip (gfx950 device code).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace stl {
+
+constexpr uint32_t kBlock = 256;          // threads per workgroup (4 waves)
+constexpr uint32_t kTableQuads = 9 * 9;   // 9 cached entries x 9 uint4 (144 B each)
+// workspace bytes per resident workgroup: 256 lanes x 81 x 16 B = 324 KiB
+constexpr size_t kWsBytesPerBlock = (size_t)kBlock * kTableQuads * 16;
+
+const void* kernel_verify_msg32();
+hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
+                         uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
+                         hipStream_t stream);
+hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t* m, const uint64_t* moff,
+                           const uint64_t* mlen, uint32_t n, uint8_t* k_out, hipStream_t stream);
+hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
+                          hipStream_t stream);
+hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
+                       uint32_t grid, hipStream_t stream);
+
+}  // namespace stl

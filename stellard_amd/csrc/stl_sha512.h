@@ -70,6 +70,7 @@ STL_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
     const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
     const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    STL_FE_FENCE();  // one round per scheduling region: bounds register pressure
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;

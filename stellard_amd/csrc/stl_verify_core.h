@@ -145,6 +145,7 @@ STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8]
   ge_p1p1_to_p3(p3, t);
   ge_p3_to_cached(c, p3);
   tab.store(2, c);
+#pragma unroll 1
   for (int e = 3; e <= 8; ++e) {
     ge_add_cached(t, p3, c1);
     ge_p1p1_to_p3(p3, t);
@@ -160,6 +161,7 @@ STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8]
   ge_p3_0(acc);
   ge_p2 acc2;
   uint32_t wa = 0, wb = 0;
+#pragma unroll 1
   for (int i = 63; i >= 0; --i) {
     if ((i & 7) == 7) {
       // fetch the next packed word (digits 8m..8m+7) by shifting the word array

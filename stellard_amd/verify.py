@@ -1,0 +1,140 @@
+"""Python mirror of stellard's signature-check interface over libstl.
+
+Reference interface being mirrored (hfeeki/stellard):
+  * RippleAddress::verifySignature(uint256 const&, Blob const&)
+      src/ripple_data/protocol/RippleAddress.cpp:190-200
+      -> throws std::runtime_error("bad inputs to verifySignature") when the
+         key is not 32 bytes or the signature not 64 bytes (:192-194);
+         returns crypto_sign_verify_detached(...) == 0 && S < L.
+  * StellarPublicKey::verifySignature  src/ripple_data/crypto/StellarPublicKey.cpp:67-77
+  * SerializedTransaction::checkSign(const RippleAddress&)
+      src/ripple_app/misc/SerializedTransaction.cpp:220-230 (any exception -> false)
+
+Every call goes to the gfx950 kernels through the C ABI; nothing here
+verifies on the CPU.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+POLICY_SODIUM_1_0_18 = N.STL_POLICY_SODIUM_1_0_18
+POLICY_STELLARD_1_0_0 = N.STL_POLICY_STELLARD_1_0_0
+
+
+class BadInputs(RuntimeError):
+    """std::runtime_error("bad inputs to verifySignature") (RippleAddress.cpp:193)."""
+
+
+def _buf(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def init(device_count=0, first_device=0):
+    class Cfg(ctypes.Structure):
+        _fields_ = [("struct_size", ctypes.c_uint32), ("device_count", ctypes.c_int32),
+                    ("first_device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+    cfg = Cfg(ctypes.sizeof(Cfg), device_count, first_device, 0)
+    return N.check(N.load().stl_init(ctypes.byref(cfg)), "stl_init")
+
+
+def verify_signature(hash32, sig, pk):
+    """RippleAddress::verifySignature: bool, raises BadInputs on size mismatch."""
+    pk, sig, hash32 = bytes(pk), bytes(sig), bytes(hash32)
+    if len(pk) != 32 or len(sig) != 64:
+        raise BadInputs("bad inputs to verifySignature")
+    rc = N.load().stl_ed25519_verify_detached(sig, hash32, len(hash32), pk)
+    if rc == 0:
+        return True
+    if rc == -1:
+        return False
+    raise N.StlError(rc, "stl_ed25519_verify_detached")
+
+
+def crypto_sign_verify_detached(sig, m, pk):
+    """libsodium call surface: 0 accept / -1 reject (+ stellard's S<L)."""
+    sig, m, pk = bytes(sig), bytes(m), bytes(pk)
+    if len(sig) != 64 or len(pk) != 32:
+        return -1
+    rc = N.load().stl_ed25519_verify_detached(sig, m, len(m), pk)
+    if rc in (0, -1):
+        return rc
+    raise N.StlError(rc, "stl_ed25519_verify_detached")
+
+
+def unpack_bitmap(bitmap, n):
+    return np.unpackbits(np.frombuffer(bytes(bitmap), dtype=np.uint8), bitorder="little")[:n].astype(bool)
+
+
+def verify_batch(sig, msg, pk, policy=POLICY_SODIUM_1_0_18):
+    """Batch RippleAddress::verifySignature over host arrays -> bool[n]."""
+    sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 64)
+    msg = np.ascontiguousarray(msg, dtype=np.uint8).reshape(-1, 32)
+    pk = np.ascontiguousarray(pk, dtype=np.uint8).reshape(-1, 32)
+    n = sig.shape[0]
+    if msg.shape[0] != n or pk.shape[0] != n:
+        raise ValueError("sig/msg/pk batch sizes differ")
+    bitmap = np.zeros((n + 7) // 8, dtype=np.uint8)
+    N.check(N.load().stl_ed25519_verify_batch(_buf(sig), _buf(msg), _buf(pk), n, _buf(bitmap), policy),
+            "stl_ed25519_verify_batch")
+    return unpack_bitmap(bitmap, n)
+
+
+def tx_verify_batch(preimages, sig, pk, policy=POLICY_SODIUM_1_0_18):
+    """Batch checkSign: preimages is a list of bytes ("STX\\0" || fields)."""
+    n = len(preimages)
+    lens = np.array([len(p) for p in preimages], dtype=np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(bytes(p) for p in preimages) or b"\0", dtype=np.uint8).copy()
+    sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 64)
+    pk = np.ascontiguousarray(pk, dtype=np.uint8).reshape(-1, 32)
+    bitmap = np.zeros((n + 7) // 8, dtype=np.uint8)
+    N.check(N.load().stl_tx_verify_batch(_buf(blob), _buf(offs), _buf(lens), _buf(sig), _buf(pk), n,
+                                         _buf(bitmap), policy), "stl_tx_verify_batch")
+    return unpack_bitmap(bitmap, n)
+
+
+# ---- device-resident (torch tensors as HBM buffers; torch is plumbing only) ----
+
+def _stream_ptr(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def verify_batch_device(sig, msg, pk, out_words=None, policy=POLICY_SODIUM_1_0_18, stream=None):
+    """sig (n,64) / msg (n,32) / pk (n,32) uint8 CUDA tensors -> int64[ceil(n/64)]
+    bitmap words (async on ``stream``)."""
+    import torch
+    n = sig.shape[0]
+    if out_words is None:
+        out_words = torch.empty((n + 63) // 64, dtype=torch.int64, device=sig.device)
+    for t in (sig, msg, pk, out_words):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("device entry point needs contiguous CUDA tensors")
+    N.check(N.load().stl_ed25519_verify_batch_device(
+        ctypes.c_void_p(sig.data_ptr()), ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(pk.data_ptr()), n,
+        ctypes.c_void_p(out_words.data_ptr()), policy, _stream_ptr(stream)), "stl_ed25519_verify_batch_device")
+    return out_words
+
+
+def sign_batch_device(seed, msg, stream=None):
+    """RFC 8032 keypair(seed) + detached signature over msg, on the GPU.
+    seed (n,32), msg (n,32) uint8 CUDA tensors -> (pk (n,32), sig (n,64))."""
+    import torch
+    n = seed.shape[0]
+    pk = torch.empty((n, 32), dtype=torch.uint8, device=seed.device)
+    sig = torch.empty((n, 64), dtype=torch.uint8, device=seed.device)
+    N.check(N.load().stl_ed25519_sign_batch_device(
+        ctypes.c_void_p(seed.data_ptr()), ctypes.c_void_p(msg.data_ptr()), n, ctypes.c_void_p(pk.data_ptr()),
+        ctypes.c_void_p(sig.data_ptr()), _stream_ptr(stream)), "stl_ed25519_sign_batch_device")
+    return pk, sig
+
+
+def words_to_bool(words, n):
+    """int64 bitmap words (torch or numpy) -> bool[n] numpy."""
+    arr = words.cpu().numpy() if hasattr(words, "cpu") else np.asarray(words)
+    return np.unpackbits(arr.astype("<i8").view(np.uint8), bitorder="little")[:n].astype(bool)

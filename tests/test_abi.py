@@ -1,0 +1,49 @@
+"""The C-ABI library loads and exports every symbol include/stl.h declares
+(no compute calls: this runs without a GPU)."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "stl.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(stl_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points():
+    syms = declared_symbols()
+    for s in ("stl_init", "stl_ed25519_verify_detached", "stl_ed25519_verify_batch", "stl_tx_verify_batch",
+              "stl_ed25519_verify_batch_device"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from stellard_amd import _native
+    lib = _native.load()
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing
+    bound = {name for name, _, _ in _native.SYMBOLS}
+    assert set(declared_symbols()) == bound
+
+
+def test_library_is_gfx950_code_object():
+    from stellard_amd import _native
+    with open(_native.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+def test_no_cpu_verify_without_gpu():
+    """Without a GPU the library reports ENODEV -- it never verifies on the host."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from stellard_amd import _native
+    lib = _native.load()
+    rc = lib.stl_ed25519_verify_detached(bytes(64), bytes(32), 32, bytes(32))
+    assert rc == _native.STL_ENODEV

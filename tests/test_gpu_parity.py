@@ -1,0 +1,228 @@
+"""GPU parity tests: the gfx950 kernels, called through the C ABI (libstl.so),
+against the golden vectors (expected bits from libsodium 1.0.18) and the CPU
+oracle (oracle/stl_oracle.c) on the same seeded inputs.  Bit-exact: any
+differing accept bit fails.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def stl(torch_cuda):
+    from stellard_amd import verify
+    verify.init()
+    return verify
+
+
+def _golden_arrays(golden):
+    return golden["sig"], golden["msg"], golden["pk"]
+
+
+@pytest.mark.parametrize("policy,key", [(0, "expected_sodium_1_0_18"), (1, "expected_stellard_1_0_0_unpinned")])
+def test_golden_host_batch(stl, golden, policy, key):
+    sig, msg, pk = _golden_arrays(golden)
+    got = stl.verify_batch(sig, msg, pk, policy=policy)
+    exp = golden[key].astype(bool)
+    bad = np.nonzero(got != exp)[0]
+    names = golden["class_names"]
+    assert bad.size == 0, [(int(i), str(names[golden["cls"][i]]), bool(got[i])) for i in bad[:20]]
+
+
+def test_golden_device_batch(stl, golden, torch_cuda):
+    torch = torch_cuda
+    sig, msg, pk = _golden_arrays(golden)
+    n = sig.shape[0]
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (sig, msg, pk)]
+    words = stl.verify_batch_device(*d)
+    torch.cuda.synchronize()
+    got = stl.words_to_bool(words, n)
+    assert np.array_equal(got, golden["expected_sodium_1_0_18"].astype(bool))
+
+
+def test_golden_per_class_counts(stl, golden):
+    """Adversarial classes reject exactly as libsodium does."""
+    sig, msg, pk = _golden_arrays(golden)
+    got = stl.verify_batch(sig, msg, pk)
+    exp = golden["expected_sodium_1_0_18"].astype(bool)
+    for c, name in enumerate(golden["class_names"]):
+        m = golden["cls"] == c
+        assert int(got[m].sum()) == int(exp[m].sum()), str(name)
+
+
+def test_single_verify_detached(stl, golden, oracle):
+    sig, msg, pk = _golden_arrays(golden)
+    exp = golden["expected_sodium_1_0_18"].astype(bool)
+    for i in list(range(0, sig.shape[0], 97)) + [sig.shape[0] - 1]:
+        assert stl.verify_signature(msg[i].tobytes(), sig[i].tobytes(), pk[i].tobytes()) == bool(exp[i])
+    with pytest.raises(stl.BadInputs):
+        stl.verify_signature(bytes(32), bytes(63), bytes(32))
+    with pytest.raises(stl.BadInputs):
+        stl.verify_signature(bytes(32), bytes(64), bytes(33))
+
+
+def test_verify_detached_variable_length(stl, oracle):
+    rng = np.random.default_rng(7)
+    for mlen in (0, 1, 31, 33, 64, 111, 112, 128, 239, 1000):
+        seed = rng.bytes(32)
+        pkb, sk = oracle.keypair(seed)
+        m = rng.bytes(mlen)
+        s = oracle.sign(m, sk)
+        assert stl.crypto_sign_verify_detached(s, m, pkb) == 0, mlen
+        bad = bytearray(s)
+        bad[5] ^= 4
+        assert stl.crypto_sign_verify_detached(bytes(bad), m, pkb) == -1, mlen
+
+
+def test_sign_kernel_matches_oracle(stl, oracle, torch_cuda):
+    """GPU RFC 8032 signer (synthetic-data generator) is byte-identical to the
+    oracle signer (deterministic signatures)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    n = 300
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pk, sig = stl.sign_batch_device(torch.from_numpy(seeds).cuda(), torch.from_numpy(msgs).cuda())
+    pk, sig = pk.cpu().numpy(), sig.cpu().numpy()
+    for i in range(0, n, 7):
+        opk, osk = oracle.keypair(seeds[i].tobytes())
+        assert pk[i].tobytes() == opk
+        assert sig[i].tobytes() == oracle.sign(msgs[i].tobytes(), osk)
+
+
+def _gpu_signed(stl, torch, n, seed):
+    rng = np.random.default_rng(seed)
+    seeds = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    pk, sig = stl.sign_batch_device(seeds, msgs)
+    return sig, msgs, pk
+
+
+def _mutate(sig, msg, pk, rng):
+    """Mix of SURVEY App. B mutations on ~30% of the rows (host numpy arrays)."""
+    n = sig.shape[0]
+    sig, msg, pk = sig.copy(), msg.copy(), pk.copy()
+    kinds = rng.integers(0, 10, n)
+    for i in np.nonzero(rng.random(n) < 0.3)[0]:
+        k = kinds[i]
+        if k == 0:
+            msg[i, rng.integers(32)] ^= 1 << rng.integers(8)
+        elif k == 1:
+            sig[i, rng.integers(32)] ^= 1 << rng.integers(8)
+        elif k == 2:
+            sig[i, 32 + rng.integers(31)] ^= 1 << rng.integers(8)
+        elif k == 3:  # S + L
+            S = int.from_bytes(sig[i, 32:].tobytes(), "little") + L
+            sig[i, 32:] = np.frombuffer(S.to_bytes(32, "little"), np.uint8)
+        elif k == 4:
+            sig[i, 63] |= 0xE0
+        elif k == 5:
+            pk[i, 31] ^= 0x80
+        elif k == 6:
+            pk[i] = np.frombuffer(bytes([1]) + bytes(31), np.uint8)
+        elif k == 7:
+            sig[i, :32] = np.frombuffer(bytes([1]) + bytes(31), np.uint8)
+        elif k == 8:
+            pk[i, rng.integers(32)] ^= 1 << rng.integers(8)
+        else:
+            pk[i] = rng.integers(0, 256, 32, dtype=np.uint8)
+    return sig, msg, pk
+
+
+@pytest.mark.parametrize("policy", [0, 1])
+def test_random_mutations_vs_oracle(stl, oracle, torch_cuda, policy):
+    torch = torch_cuda
+    n = 12288
+    sig, msg, pk = _gpu_signed(stl, torch, n, 1234)
+    rng = np.random.default_rng(99)
+    sig, msg, pk = _mutate(sig.cpu().numpy(), msg.cpu().numpy(), pk.cpu().numpy(), rng)
+    exp = oracle.verify_batch(sig, msg, pk, policy=policy, threads=16)
+    got = stl.verify_batch(sig, msg, pk, policy=policy)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, bad[:20]
+    assert 0.5 < exp.mean() < 0.95
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1023, 4097])
+def test_ragged_sizes(stl, golden, n):
+    sig, msg, pk = _golden_arrays(golden)
+    idx = np.arange(n) % sig.shape[0]
+    got = stl.verify_batch(sig[idx], msg[idx], pk[idx])
+    assert np.array_equal(got, golden["expected_sodium_1_0_18"][idx].astype(bool))
+
+
+def test_empty_batch(stl):
+    z = np.zeros((0, 64), np.uint8)
+    assert stl.verify_batch(z, np.zeros((0, 32), np.uint8), np.zeros((0, 32), np.uint8)).size == 0
+
+
+def test_full_size_valid_batch(stl, oracle, torch_cuda):
+    """configs[1]: 1,048,576 signatures, all valid -> every bit set; a seeded
+    sample of 8192 rows re-checked by the oracle; the bitmap is independent of
+    how the batch is split (device API, one call vs. 4 calls)."""
+    torch = torch_cuda
+    n = 1 << 20
+    sig, msg, pk = _gpu_signed(stl, torch, n, 0x5EED0002)
+    words = stl.verify_batch_device(sig, msg, pk)
+    torch.cuda.synchronize()
+    got = stl.words_to_bool(words, n)
+    assert got.all(), int((~got).sum())
+    # a mutated copy: flip one S bit in every 97th row
+    sig2 = sig.clone()
+    sig2[::97, 40] ^= 1
+    w2 = stl.verify_batch_device(sig2, msg, pk)
+    q = n // 4
+    parts = [stl.verify_batch_device(sig2[i * q:(i + 1) * q].contiguous(), msg[i * q:(i + 1) * q].contiguous(),
+                                     pk[i * q:(i + 1) * q].contiguous()) for i in range(4)]
+    torch.cuda.synchronize()
+    b2 = stl.words_to_bool(w2, n)
+    assert np.array_equal(b2, np.concatenate([stl.words_to_bool(p, q) for p in parts]))
+    expect = np.ones(n, bool)
+    expect[::97] = False
+    assert np.array_equal(b2, expect)
+    rng = np.random.default_rng(5)
+    sample = rng.choice(n, 8192, replace=False)
+    s_np, m_np, p_np = sig2.cpu().numpy()[sample], msg.cpu().numpy()[sample], pk.cpu().numpy()[sample]
+    assert np.array_equal(b2[sample], oracle.verify_batch(s_np, m_np, p_np, threads=16))
+
+
+def test_tx_verify_batch_vs_oracle(stl, oracle):
+    """checkSign path: SHA512Half(preimage) on the GPU, then verify."""
+    rng = np.random.default_rng(21)
+    n = 600
+    pre, sigs, pks = [], [], []
+    seed_keys = [oracle.keypair(rng.bytes(32)) for _ in range(16)]
+    for i in range(n):
+        ln = int(np.exp(rng.uniform(np.log(100), np.log(4096))))
+        p = b"STX\x00" + rng.bytes(ln - 4)
+        pkb, sk = seed_keys[i % 16]
+        h = hashlib.sha512(p).digest()[:32]
+        s = bytearray(oracle.sign(h, sk))
+        if i % 5 == 0:
+            s[rng.integers(64)] ^= 1 << int(rng.integers(8))
+        if i % 7 == 0:
+            p = p[:-1] + bytes([p[-1] ^ 1])
+        pre.append(p)
+        sigs.append(bytes(s))
+        pks.append(pkb)
+    sig = np.frombuffer(b"".join(sigs), np.uint8).reshape(n, 64)
+    pk = np.frombuffer(b"".join(pks), np.uint8).reshape(n, 32)
+    exp = oracle.tx_verify_batch(pre, sig, pk, threads=16)
+    got = stl.tx_verify_batch(pre, sig, pk)
+    assert np.array_equal(got, exp)
+    assert 0.5 < exp.mean() < 0.9
