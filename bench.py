@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 17)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 19)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
