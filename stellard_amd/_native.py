@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstl.so")
+LIB_PATH = os.environ.get("STL_LIB_PATH") or os.path.join(_HERE, "libstl.so")
 
 STL_OK = 0
 STL_EINVAL = -22

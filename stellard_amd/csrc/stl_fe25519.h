@@ -102,27 +102,28 @@ STL_HD void fe_cmov(fe& h, const fe& a, const fe& b, bool c) {
   for (int i = 0; i < 9; ++i) h.v[i] = c ? b.v[i] : a.v[i];
 }
 
-// Product-scanning reduction shared by fe_mul / fe_sq.  COL(k) yields the
-// 64-bit sum of the partial products of column k (k = 0..16, each
-// < 63 * 2^58).  The high columns 9..16 are produced first and normalised to
-// 29-bit digits on the fly; each then folds into column k-9 with weight
-// 2^261 == 64 * 19 = 1216 (mod p).  Only one 64-bit column accumulator is live
-// at a time (register pressure of the verify kernel).
+// Product-scanning reduction shared by fe_mul / fe_sq.  COL(k, init) yields
+// init + the 64-bit sum of the partial products of column k (k = 0..16, each
+// sum < 63 * 2^58), so every column is one v_mad_u64_u32 chain that starts
+// from the incoming carry.  The high columns 9..16 are produced first and
+// normalised to 29-bit digits on the fly; digit k+9 then enters column k as one
+// more mad with weight 2^261 == 64 * 19 = 1216 (mod p).  Only one 64-bit
+// column accumulator is live at a time (register pressure of the verify kernel).
 #define STL_FE_REDUCE_COLUMNS(h, COL)                                   \
   do {                                                                  \
     uint32_t hi_[8];                                                    \
     uint64_t carry_ = 0;                                                \
     _Pragma("unroll") for (int k = 9; k < 17; ++k) {                    \
-      const uint64_t t_ = COL(k) + carry_;                              \
+      const uint64_t t_ = COL(k, carry_);                               \
       hi_[k - 9] = (uint32_t)t_ & M29;                                  \
       carry_ = t_ >> 29;                                                \
     }                                                                   \
-    const uint64_t top_ = carry_; /* weight 2^(29*17) */                \
+    const uint64_t top_ = carry_ * 1216u; /* weight 2^(29*17): into col 8 */ \
     carry_ = 0;                                                         \
     _Pragma("unroll") for (int k = 0; k < 9; ++k) {                     \
-      const uint64_t f_ = k < 8 ? (uint64_t)hi_[k < 8 ? k : 0] * 1216u  \
-                                : top_ * 1216u;                         \
-      const uint64_t t_ = COL(k) + f_ + carry_;                         \
+      const uint64_t init_ = k < 8 ? (uint64_t)hi_[k < 8 ? k : 0] * 1216u + carry_ \
+                                   : top_ + carry_;                     \
+      const uint64_t t_ = COL(k, init_);                                \
       (h).v[k] = (uint32_t)t_ & M29;                                    \
       carry_ = t_ >> 29;                                                \
     }                                                                   \
@@ -131,8 +132,7 @@ STL_HD void fe_cmov(fe& h, const fe& a, const fe& b, bool c) {
     (h).v[1] += (uint32_t)(u_ >> 29);                                   \
   } while (0)
 
-STL_HD uint64_t fe_mul_col(const fe& a, const fe& b, int k) {
-  uint64_t acc = 0;
+STL_HD uint64_t fe_mul_col(const fe& a, const fe& b, int k, uint64_t acc) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int j = k - i;
@@ -143,22 +143,21 @@ STL_HD uint64_t fe_mul_col(const fe& a, const fe& b, int k) {
 }
 
 // d = 2a (precomputed); column k of a^2 = sum_{i<j} d_i a_j + [k even] a_{k/2}^2
-STL_HD uint64_t fe_sq_col(const fe& a, const uint32_t d[9], int k) {
-  uint64_t acc = 0;
+STL_HD uint64_t fe_sq_col(const fe& a, const uint32_t d[9], int k, uint64_t acc) {
+  if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int j = k - i;
     if (j <= i || j > 8) continue;
     acc += (uint64_t)d[i] * a.v[j];
   }
-  if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
   return acc;
 }
 
 STL_HD void fe_mul(fe& h, const fe& a, const fe& b) {
   STL_BOUND_MUL(a, b);
   const fe a_ = a, b_ = b;  // h may alias a or b
-#define STL_MUL_COL(k) fe_mul_col(a_, b_, (k))
+#define STL_MUL_COL(k, init) fe_mul_col(a_, b_, (k), (init))
   STL_FE_REDUCE_COLUMNS(h, STL_MUL_COL);
 #undef STL_MUL_COL
   STL_FE_FENCE();
@@ -170,7 +169,7 @@ STL_HD void fe_sq(fe& h, const fe& a) {
   uint32_t d[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) d[i] = a_.v[i] << 1;  // alpha <= 2.64 => fits 32 bits
-#define STL_SQ_COL(k) fe_sq_col(a_, d, (k))
+#define STL_SQ_COL(k, init) fe_sq_col(a_, d, (k), (init))
   STL_FE_REDUCE_COLUMNS(h, STL_SQ_COL);
 #undef STL_SQ_COL
   STL_FE_FENCE();

@@ -39,9 +39,18 @@ __device__ __forceinline__ void st8(uint8_t* p, const uint32_t w[8]) {
   q[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
+// Copy the 128-entry affine base table (14 KiB) into LDS once per workgroup.
+__device__ __forceinline__ void stage_base_table(uint32_t* sB) {
+  const uint32_t* g = &kBaseNiels[0][0];
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(kBaseTableEntries * kBaseNielsWords); i += kBlock) sB[i] = g[i];
+  __syncthreads();
+}
+
 __device__ __forceinline__ TableView lane_table(uint4* ws) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  return TableView{ws + ((size_t)blockIdx.x * (kBlock / 64) + wave) * kTableQuads * 64 + lane, 64};
+  // per-lane contiguous entries: one lookup touches 2-3 whole 128-B lines of
+  // its own lane instead of 16 B of nine lines shared by lanes with other digits
+  return TableView{ws + (((size_t)blockIdx.x * (kBlock / 64) + wave) * 64 + lane) * kTableQuads, 1};
 }
 
 template <bool PRE_K>
@@ -50,6 +59,8 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_kern
                                                         const uint8_t* __restrict__ pk, uint32_t n,
                                                         uint64_t* __restrict__ bitmap, uint32_t policy,
                                                         uint4* __restrict__ ws) {
+  __shared__ uint32_t sB[kBaseTableEntries * kBaseNielsWords];
+  stage_base_table(sB);
   const TableView tv = lane_table(ws);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -61,8 +72,7 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_kern
     ld8(S, sig + 64 * j + 32);
     ld8(A, pk + 32 * j);
     ld8(M, msg_or_k + 32 * j);
-    bool ok = PRE_K ? verify_with_k(R, S, A, M, policy, tv, kBaseNiels)
-                    : verify_msg32(R, S, A, M, policy, tv, kBaseNiels);
+    bool ok = PRE_K ? verify_with_k(R, S, A, M, policy, tv, sB) : verify_msg32(R, S, A, M, policy, tv, sB);
     ok = ok && live;
     const uint64_t word = __ballot(ok);
     const uint32_t wbase = base + wave * 64;
@@ -118,6 +128,8 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
                                                       const uint8_t* __restrict__ msg, uint32_t n,
                                                       uint8_t* __restrict__ pk_out, uint8_t* __restrict__ sig_out,
                                                       uint4* __restrict__ ws) {
+  __shared__ uint32_t sB[kBaseTableEntries * kBaseNielsWords];
+  stage_base_table(sB);
   const TableView tv = lane_table(ws);
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     const uint32_t i = base + threadIdx.x;
@@ -142,7 +154,7 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
     ge_p3_0(id);
     ge_p2 P;
     uint32_t A[8];
-    double_scalarmult(P, id, zero, a_red, tv, kBaseNiels);  // A = [a]B
+    double_scalarmult(P, id, zero, a_red, tv, sB);  // A = [a]B
     ge_tobytes(A, P);
     // r = SHA-512(h[32..63] || M) mod L
 #pragma unroll
@@ -153,7 +165,7 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
     uint32_t rh[16], r[8], R[8];
     sha512_short(rh, pre, 16);
     sc_reduce64(r, rh);
-    double_scalarmult(P, id, zero, r, tv, kBaseNiels);      // R = [r]B
+    double_scalarmult(P, id, zero, r, tv, sB);      // R = [r]B
     ge_tobytes(R, P);
     uint32_t kh[16], k[8], S[8];
     sha512_hram32(kh, R, A, M);

@@ -117,6 +117,25 @@ STL_HD void sc_recode16(uint32_t packed[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-256 recoding of a scalar < 2^253 into 32 digits in [-128, 127]
+// (digit 31 in [0, 32]), packed as int8, 4 digits per word (digit 4m+j in
+// byte j of word m).  Drives the [S]B part with the 128-entry base table.
+STL_HD void sc_recode256(uint32_t packed[8], const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int e = (int)((s[m] >> (8 * j)) & 255u) + carry;
+      carry = (e + 128) >> 8;
+      e -= carry << 8;
+      word |= ((uint32_t)e & 255u) << (8 * j);
+    }
+    packed[m] = word;
+  }
+}
+
 // out = (a*b + c) mod L   (signing: S = r + k*a)
 STL_HD void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]) {
   uint32_t p[16];

@@ -68,9 +68,8 @@ STL_HD bool verify_prechecks(const uint32_t R[8], const uint32_t S[8], const uin
 }
 
 // Per-lane table of cached multiples e*(-A), e = 0..8, 9 x uint4 per entry.
-// LaneStride = distance (in uint4) between consecutive lanes' copies of the
-// same (entry, quad): 64 on the device (one wave's lanes interleaved), 1 for
-// the host test harness.
+// stride = distance (in uint4) between consecutive quads of one entry; the
+// kernel keeps each lane's 1296-byte table contiguous (stride 1).
 struct TableView {
   uint4* base;
   int stride;
@@ -109,15 +108,16 @@ struct TableView {
   }
 };
 
-STL_HD void load_base_niels(ge_niels& n, const uint32_t (*tab)[27], int absd) {
-  const int idx = absd > 0 ? absd - 1 : 0;
+// j*B from the 128-entry affine table (row-major, kBaseNielsWords per row):
+// absd = |digit| in [0, 128]; digit 0 selects the identity (1, 1, 0).
+STL_HD void load_base_niels(ge_niels& n, const uint32_t* tab, int absd) {
+  const uint32_t* row = tab + (absd > 0 ? absd - 1 : 0) * 28;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    n.ypx.v[i] = tab[idx][i];
-    n.ymx.v[i] = tab[idx][9 + i];
-    n.xy2d.v[i] = tab[idx][18 + i];
+    n.ypx.v[i] = row[i];
+    n.ymx.v[i] = row[9 + i];
+    n.xy2d.v[i] = row[18 + i];
   }
-  // digit 0: the identity (1, 1, 0)
   ge_niels id;
   fe_1(id.ypx);
   fe_1(id.ymx);
@@ -129,8 +129,12 @@ STL_HD void load_base_niels(ge_niels& n, const uint32_t (*tab)[27], int absd) {
 }
 
 // R' = [k](-A) + [S]B  with k, S < 2^253.  negA is the decompressed -A.
+// Joint Straus over 64 nibble positions (shared doublings): k in signed
+// radix 16 (an A-add at every position, 9-entry per-lane table), S in signed
+// radix 256 (a B-add at every even position, 128-entry shared table
+// `btab`, LDS on the device).
 STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8], const uint32_t S[8],
-                              const TableView& tab, const uint32_t (*bniels)[27]) {
+                              const TableView& tab, const uint32_t* btab) {
   // ---- table of e*(-A), e = 0..8 ----
   ge_cached c1, c;
   ge_cached_0(c);
@@ -152,26 +156,26 @@ STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8]
     ge_p3_to_cached(c, p3);
     tab.store(e, c);
   }
-  // ---- signed radix-16 digits ----
+  // ---- signed digits ----
   uint32_t kd[8], sd[8];
   sc_recode16(kd, k);
-  sc_recode16(sd, S);
-  // ---- main loop: 64 digit positions, most significant first ----
+  sc_recode256(sd, S);
+  // ---- main loop: 64 nibble positions, most significant first ----
   ge_p3 acc;
   ge_p3_0(acc);
   ge_p2 acc2;
   uint32_t wa = 0, wb = 0;
 #pragma unroll 1
   for (int i = 63; i >= 0; --i) {
-    if ((i & 7) == 7) {
-      // fetch the next packed word (digits 8m..8m+7) by shifting the word array
+    if ((i & 7) == 7) {  // next 8 radix-16 digits of k
       wa = kd[7];
+#pragma unroll
+      for (int m = 7; m > 0; --m) kd[m] = kd[m - 1];
+    }
+    if ((i & 7) == 6) {  // next 4 radix-256 digits of S
       wb = sd[7];
 #pragma unroll
-      for (int m = 7; m > 0; --m) {
-        kd[m] = kd[m - 1];
-        sd[m] = sd[m - 1];
-      }
+      for (int m = 7; m > 0; --m) sd[m] = sd[m - 1];
     }
     if (i != 63) {
 #pragma unroll 1
@@ -182,30 +186,34 @@ STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8]
       ge_p2_dbl(t, acc2);
       ge_p1p1_to_p3(acc, t);
     }
+    // A digit (every position)
     const int da = (int32_t)wa >> 28;
-    const int db = (int32_t)wb >> 28;
     wa <<= 4;
-    wb <<= 4;
-    // A digit
     const int ada = da < 0 ? -da : da;
     tab.load(ada > 8 ? 8 : ada, c);
     ge_cached_cneg(c, da < 0);
     ge_add_cached(t, acc, c);
-    ge_p1p1_to_p3(acc, t);
-    // B digit
-    const int adb = db < 0 ? -db : db;
-    ge_niels n;
-    load_base_niels(n, bniels, adb > 8 ? 8 : adb);
-    ge_niels_cneg(n, db < 0);
-    ge_madd(t, acc, n);
-    ge_p1p1_to_p2(acc2, t);
+    if (i & 1) {
+      ge_p1p1_to_p2(acc2, t);
+    } else {
+      // B digit (even positions: bits 4i .. 4i+7)
+      ge_p1p1_to_p3(acc, t);
+      const int db = (int32_t)wb >> 24;
+      wb <<= 8;
+      const int adb = db < 0 ? -db : db;
+      ge_niels n;
+      load_base_niels(n, btab, adb > 128 ? 128 : adb);
+      ge_niels_cneg(n, db < 0);
+      ge_madd(t, acc, n);
+      ge_p1p1_to_p2(acc2, t);
+    }
   }
   out = acc2;
 }
 
 // Full check for one signature given k = H(R||A||M) mod L (8 words).
 STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
-                          uint32_t policy, const TableView& tab, const uint32_t (*bniels)[27]) {
+                          uint32_t policy, const TableView& tab, const uint32_t* bniels) {
   bool ok = verify_prechecks(R, S, A, policy);
   ge_p3 negA;
   ok = ge_frombytes_negate_vartime(negA, A) && ok;
@@ -228,7 +236,7 @@ STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32
 
 // Fixed 32-byte message (the stellard signing hash): k computed in-lane.
 STL_HD bool verify_msg32(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t M[8],
-                         uint32_t policy, const TableView& tab, const uint32_t (*bniels)[27]) {
+                         uint32_t policy, const TableView& tab, const uint32_t* bniels) {
   uint32_t h[16], k[8];
   sha512_hram32(h, R, A, M);
   sc_reduce64(k, h);

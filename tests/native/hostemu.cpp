@@ -50,7 +50,7 @@ uint64_t hostemu_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint
     load8(S, sig + 64 * i + 32);
     load8(A, pk + 32 * i);
     load8(M, msg + 32 * i);
-    if (stl::verify_msg32(R, S, A, M, policy, tv, stl::kBaseNielsHost)) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+    if (stl::verify_msg32(R, S, A, M, policy, tv, &stl::kBaseNielsHost[0][0])) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
   }
   return g_bound_viol.load();
 }
