@@ -94,6 +94,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
+    from stellard_amd import shard
     from stellard_amd import verify as V
 
     V.init(device_count=1, first_device=torch.cuda.current_device())
@@ -107,13 +108,17 @@ def main():
     pk, sig = V.sign_batch_device(seeds, msgs)
     torch.cuda.synchronize()
     words = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
-    gathered = [torch.empty_like(words) for _ in range(world)] if world > 1 else None
+    full_words = None
     stream = torch.cuda.current_stream()
+
+    def gather():
+        # rank r holds global indices [r*n, (r+1)*n): shard.shard_range(n*world, r, world)
+        return shard.gather_bitmap_words(words, n * world, world, dist)
 
     def step():
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
         if world > 1:
-            dist.all_gather(gathered, words)
+            gather()
 
     for _ in range(args.warmup):
         step()
@@ -133,7 +138,7 @@ def main():
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
         ev[k][1].record(stream)
         if world > 1:
-            dist.all_gather(gathered, words)
+            full_words = gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -144,8 +149,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, kern_ms = float(t[0]), float(t[1])
     if world > 1:
-        full = V.words_to_bool(torch.cat(gathered), n * world)
-        assert full.all()
+        assert V.words_to_bool(full_words, n * world).all()
 
     if rank == 0:
         total = n * world * args.steps
