@@ -95,7 +95,7 @@ int stream_workspace(Device& d, hipStream_t s, uint4** ws) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
   auto& slot = d.stream_ws[s];
   if (!slot) slot.reset(new DevBuf());
-  int rc = slot->ensure(stl::kWsBytesPerBlock * d.grid);
+  int rc = slot->ensure(stl::verify_ws_bytes(d.grid));
   if (rc) return rc;
   *ws = static_cast<uint4*>(slot->p);
   return STL_OK;
@@ -124,7 +124,7 @@ int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t
   STL_TRY(hipSetDevice(d.ordinal));
   int rc;
   const size_t words = (n + 63) / 64;
-  if ((rc = d.ws.ensure(stl::kWsBytesPerBlock * d.grid)) || (rc = d.sig.ensure(n * 64)) ||
+  if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(n * 64)) ||
       (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)))
     return rc;
   hipStream_t s = d.stream;
@@ -285,7 +285,7 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
   Device& d = *g_devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
   STL_TRY(hipSetDevice(d.ordinal));
-  if ((rc = d.ws.ensure(stl::kWsBytesPerBlock * d.grid)) || (rc = d.sig.ensure(64)) || (rc = d.pk.ensure(32)) ||
+  if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(64)) || (rc = d.pk.ensure(32)) ||
       (rc = d.msg.ensure(32)) || (rc = d.bitmap.ensure(8)) || (rc = d.pre.ensure(mlen ? mlen : 1)) ||
       (rc = d.off.ensure(16)))
     return rc;

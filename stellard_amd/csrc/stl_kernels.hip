@@ -21,7 +21,7 @@
 // Occupancy target of the verify kernel (waves per SIMD); register budget =
 // 512 / waves.  Tuned on MI355X ("occupancy").
 #ifndef STL_VERIFY_WAVES_PER_SIMD
-#define STL_VERIFY_WAVES_PER_SIMD 2
+#define STL_VERIFY_WAVES_PER_SIMD 3
 #endif
 
 namespace stl {
@@ -53,30 +53,92 @@ __device__ __forceinline__ TableView lane_table(uint4* ws) {
   return TableView{ws + (((size_t)blockIdx.x * (kBlock / 64) + wave) * 64 + lane) * kTableQuads, 1};
 }
 
+__device__ __forceinline__ void ld_pre(PreState& p, const uint4* q) {
+  uint32_t w[28];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const uint4 v = q[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p.k[i] = w[i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    p.negAx.v[i] = w[8 + i];
+    p.negAy.v[i] = w[17 + i];
+  }
+  p.ok = w[26];
+  p.pad = 0;
+}
+
+__device__ __forceinline__ void st_pre(uint4* q, const PreState& p) {
+  uint32_t w[28];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = p.k[i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    w[8 + i] = p.negAx.v[i];
+    w[17 + i] = p.negAy.v[i];
+  }
+  w[26] = p.ok;
+  w[27] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Phase 1: one signature per lane -- pre-checks, k = SHA-512(R||A||M) mod L
+// (or k given, PRE_K), decompression of A.  Signatures [base, base+cnt).
 template <bool PRE_K>
-__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_kernel(const uint8_t* __restrict__ sig,
-                                                        const uint8_t* __restrict__ msg_or_k,
-                                                        const uint8_t* __restrict__ pk, uint32_t n,
-                                                        uint64_t* __restrict__ bitmap, uint32_t policy,
-                                                        uint4* __restrict__ ws) {
+__global__ __launch_bounds__(kBlock) void verify_pre_kernel(const uint8_t* __restrict__ sig,
+                                                            const uint8_t* __restrict__ msg_or_k,
+                                                            const uint8_t* __restrict__ pk, uint32_t base,
+                                                            uint32_t cnt, uint32_t policy, uint4* __restrict__ pre) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= cnt) return;
+  const size_t j = (size_t)base + t;
+  uint32_t R[8], S[8], A[8], M[8], k[8];
+  ld8(R, sig + 64 * j);
+  ld8(S, sig + 64 * j + 32);
+  ld8(A, pk + 32 * j);
+  ld8(M, msg_or_k + 32 * j);
+  if (PRE_K) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = M[i];
+  } else {
+    uint32_t h[16];
+    sha512_hram32(h, R, A, M);
+    sc_reduce64(k, h);
+  }
+  PreState p;
+  verify_phase1(p, R, S, A, k, policy);
+  st_pre(pre + (size_t)t * 7, p);
+}
+
+// Phase 2: the Straus loop, encode and compare; grid-strides over 256-signature
+// tiles of [base, base+cnt) so the per-lane table workspace is bounded by the
+// resident lanes; one ballot word per wave.
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_kernel(
+    const uint8_t* __restrict__ sig, const uint4* __restrict__ pre, uint32_t base, uint32_t cnt,
+    uint64_t* __restrict__ bitmap, uint4* __restrict__ ws) {
   __shared__ uint32_t sB[kBaseTableEntries * kBaseNielsWords];
   stage_base_table(sB);
   const TableView tv = lane_table(ws);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-    const uint32_t i = base + threadIdx.x;
-    const bool live = i < n;
-    const size_t j = live ? i : (n - 1);  // tail lanes re-read a valid element
-    uint32_t R[8], S[8], A[8], M[8];
+  for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
+    const uint32_t t = tile + threadIdx.x;
+    const bool live = t < cnt;
+    const uint32_t tt = live ? t : (cnt - 1);  // tail lanes re-read a valid element
+    const size_t j = (size_t)base + tt;
+    PreState p;
+    ld_pre(p, pre + (size_t)tt * 7);
+    uint32_t R[8], S[8];
     ld8(R, sig + 64 * j);
     ld8(S, sig + 64 * j + 32);
-    ld8(A, pk + 32 * j);
-    ld8(M, msg_or_k + 32 * j);
-    bool ok = PRE_K ? verify_with_k(R, S, A, M, policy, tv, sB) : verify_msg32(R, S, A, M, policy, tv, sB);
+    bool ok = verify_phase2(p, R, S, tv, sB);
     ok = ok && live;
     const uint64_t word = __ballot(ok);
-    const uint32_t wbase = base + wave * 64;
-    if (lane == 0 && wbase < n) bitmap[wbase >> 6] = word;
+    const uint32_t wbase = tile + wave * 64;
+    if (lane == 0 && wbase < cnt) bitmap[(base + wbase) >> 6] = word;
   }
 }
 
@@ -180,18 +242,28 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
 }
 
 // ---- host-side launchers (called from stl_api.cpp) ----
-const void* kernel_verify_msg32() { return reinterpret_cast<const void*>(&verify_kernel<false>); }
+const void* kernel_verify_msg32() { return reinterpret_cast<const void*>(&verify_main_kernel); }
 
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
                          hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  if (pre_k)
-    hipLaunchKernelGGL(verify_kernel<true>, dim3(grid), dim3(kBlock), 0, stream, sig, msg_or_k, pk, n, bitmap,
-                       policy, ws);
-  else
-    hipLaunchKernelGGL(verify_kernel<false>, dim3(grid), dim3(kBlock), 0, stream, sig, msg_or_k, pk, n, bitmap,
-                       policy, ws);
+  // ws = [per-lane tables: grid x kWsBytesPerBlock][PreState x kPreChunk]
+  uint4* tables = ws;
+  uint4* pre = ws + (size_t)grid * (kWsBytesPerBlock / 16);
+  for (uint32_t base = 0; base < n; base += kPreChunk) {
+    const uint32_t cnt = n - base < kPreChunk ? n - base : kPreChunk;
+    const dim3 g1((cnt + kBlock - 1) / kBlock);
+    if (pre_k)
+      hipLaunchKernelGGL(verify_pre_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
+                         pre);
+    else
+      hipLaunchKernelGGL(verify_pre_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
+                         policy, pre);
+    const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(verify_main_kernel, dim3(tiles < grid ? tiles : grid), dim3(kBlock), 0, stream, sig, pre,
+                       base, cnt, bitmap, tables);
+  }
   return hipGetLastError();
 }
 

@@ -211,12 +211,42 @@ STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8]
   out = acc2;
 }
 
-// Full check for one signature given k = H(R||A||M) mod L (8 words).
-STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
-                          uint32_t policy, const TableView& tab, const uint32_t* bniels) {
+// ---- two-phase form used by the gfx950 kernels ----
+// Phase 1 (short-lived, few registers): pre-checks, k, decompression of A.
+// Phase 2 (the Straus loop, register-heavy): [k](-A) + [S]B, encode, compare.
+// Splitting them into two launches keeps each kernel's register allocation to
+// what its own phase needs.  PreState is 112 bytes
+// (7 x uint4), written and read once per signature.
+struct PreState {
+  uint32_t k[8];     // H(R||A||M) mod L
+  fe negAx, negAy;   // decompressed -A, affine (Z = 1)
+  uint32_t ok;       // pre-checks && A decodes && S < L (stellard composite)
+  uint32_t pad;
+};
+static_assert(sizeof(PreState) == 112, "PreState must be 7 x uint4");
+
+STL_HD void verify_phase1(PreState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
+                          const uint32_t k[8], uint32_t policy) {
   bool ok = verify_prechecks(R, S, A, policy);
   ge_p3 negA;
   ok = ge_frombytes_negate_vartime(negA, A) && ok;
+  // stellard composite: && signatureIsCanonical (S < L), RippleAddress.cpp:198-199
+  ok = ok && sc_lt_L(S);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o.k[i] = k[i];
+  o.negAx = negA.X;
+  o.negAy = negA.Y;
+  o.ok = ok ? 1u : 0u;
+  o.pad = 0;
+}
+
+STL_HD bool verify_phase2(const PreState& p, const uint32_t R[8], const uint32_t S[8], const TableView& tab,
+                          const uint32_t* bniels) {
+  ge_p3 negA;
+  negA.X = p.negAx;
+  negA.Y = p.negAy;
+  fe_1(negA.Z);
+  fe_mul(negA.T, negA.X, negA.Y);
   // S < 2^253 is guaranteed for accepted lanes under both policies; mask so a
   // rejected lane still runs the same bounded digit range.
   uint32_t Sm[8];
@@ -224,14 +254,21 @@ STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32
   for (int i = 0; i < 8; ++i) Sm[i] = S[i];
   Sm[7] &= 0x1fffffffu;
   ge_p2 Rp;
-  double_scalarmult(Rp, negA, k, Sm, tab, bniels);
+  double_scalarmult(Rp, negA, p.k, Sm, tab, bniels);
   uint32_t enc[8];
   ge_tobytes(enc, Rp);
   bool eq = true;
 #pragma unroll
   for (int i = 0; i < 8; ++i) eq = eq && enc[i] == R[i];
-  // stellard composite: && signatureIsCanonical (S < L)
-  return ok && eq && sc_lt_L(S);
+  return p.ok != 0 && eq;
+}
+
+// Full check for one signature given k = H(R||A||M) mod L (8 words).
+STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
+                          uint32_t policy, const TableView& tab, const uint32_t* bniels) {
+  PreState p;
+  verify_phase1(p, R, S, A, k, policy);
+  return verify_phase2(p, R, S, tab, bniels);
 }
 
 // Fixed 32-byte message (the stellard signing hash): k computed in-lane.
