@@ -59,6 +59,10 @@ extern "C" {
 /* stellard's crypto_sign_check_S_lt_l (RippleAddress.cpp:226-252) is always
  * applied (composite predicate); the flag exists for ABI symmetry. */
 #define STL_REQUIRE_S_LT_L 0x2u
+/* Check every signature with full-length scalars ([S]B - [k]A, 253-bit
+ * chain) instead of the half-size-scalar equation.
+ * Same accept bits, about 1.6x slower; a cross-check / reference mode. */
+#define STL_FULL_LENGTH 0x4u
 
 typedef struct stl_config {
   uint32_t struct_size;  /* sizeof(stl_config) */

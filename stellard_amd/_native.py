@@ -20,6 +20,7 @@ STL_POLICY_SODIUM_1_0_18 = 0x0
 STL_POLICY_STELLARD_1_0_0 = 0x1
 STL_POLICY_MASK = 0x1
 STL_REQUIRE_S_LT_L = 0x2
+STL_FULL_LENGTH = 0x4
 
 # Every entry point include/stl.h declares: (name, restype, argtypes)
 _P = ctypes.c_void_p

@@ -165,10 +165,10 @@ int run_batch(const uint8_t* sig, const uint8_t* msg32, const uint8_t* pk, const
               const uint32_t* len, size_t n, uint8_t* bitmap, uint32_t flags) {
   if (n == 0) return STL_OK;
   if (!sig || !pk || !bitmap || (!msg32 && (!pre || !off || !len))) return STL_EINVAL;
-  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L)) return STL_EINVAL;
+  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) return STL_EINVAL;
   int rc = ensure_init();
   if (rc) return rc;
-  const uint32_t policy = flags & STL_POLICY_MASK;
+  const uint32_t policy = stl::kernel_mode(flags);
   const int g = (int)g_devs.size();
   if (g == 0) return STL_ENODEV;
   // one kernel launch handles up to 2^32-64 signatures per shard
@@ -311,7 +311,7 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
                                     uint64_t* d_bitmap_words, uint32_t flags, void* stream) {
   if (n == 0) return STL_OK;
   if (!d_sig || !d_msg || !d_pk || !d_bitmap_words) return STL_EINVAL;
-  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L)) return STL_EINVAL;
+  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) return STL_EINVAL;
   if (n > 0xffffffc0ull) return STL_EINVAL;
   int rc = ensure_init();
   if (rc) return rc;
@@ -321,7 +321,7 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint4* ws = nullptr;
   if ((rc = stream_workspace(d, s, &ws))) return rc;
-  STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, flags & STL_POLICY_MASK, ws,
+  STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
                              grid_for(d, n), false, s));
   return STL_OK;
 }

@@ -8,14 +8,21 @@ namespace stl {
 
 constexpr uint32_t kBlock = 256;          // threads per workgroup (4 waves)
 constexpr uint32_t kTableQuads = 9 * 9;   // 9 cached entries x 9 uint4 (144 B each)
-// workspace bytes per resident workgroup: 256 lanes x 81 x 16 B = 324 KiB
-constexpr size_t kWsBytesPerBlock = (size_t)kBlock * kTableQuads * 16;
-// verify phase-1 state (PreState, 112 B) is produced and consumed in chunks of
-// kPreChunk signatures (a multiple of 64, so chunks start on bitmap words)
+constexpr uint32_t kSlotQuads = 2 * kTableQuads;  // per-lane slot: two tables
+// workspace bytes per resident workgroup: 256 lanes x 162 x 16 B = 648 KiB
+constexpr size_t kWsBytesPerBlock = (size_t)kBlock * kSlotQuads * 16;
+// verify phase-1 state (HalfState, 224 B) is produced and consumed in chunks
+// of kPreChunk signatures (a multiple of 64, so chunks start on bitmap words),
+// plus one fallback-flag word per 64 signatures
 constexpr uint32_t kPreChunk = 1u << 20;
-constexpr size_t kPreBytes = (size_t)kPreChunk * 112;
+constexpr size_t kPreBytes = (size_t)kPreChunk * 224 + (size_t)kPreChunk / 8;
 // verify workspace for a grid of `grid` resident workgroups
 inline size_t verify_ws_bytes(uint32_t grid) { return kWsBytesPerBlock * grid + kPreBytes; }
+
+// Kernel mode word: bit 0 = policy (STL_POLICY_*), bit 8 = full-length path
+// for every lane (STL_FULL_LENGTH).
+constexpr uint32_t kModeFullLength = 0x100u;
+inline uint32_t kernel_mode(uint32_t flags) { return (flags & 0x1u) | ((flags & 0x4u) ? kModeFullLength : 0u); }
 
 const void* kernel_verify_msg32();
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,

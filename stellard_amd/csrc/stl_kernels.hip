@@ -1,19 +1,21 @@
 // stl_kernels.hip -- gfx950 kernels of libstl.
 //
-//   verify_msg32_kernel   the hot path: one Ed25519 verification per lane
+//   verify_pre_kernel     phase 1 of one Ed25519 verification per lane
 //                         (RippleAddress::verifySignature over the 32-byte
-//                         signing hash, RippleAddress.cpp:190-200), accept
-//                         bits assembled per wave with a 64-bit ballot.
-//   verify_prek_kernel    same with k = H(R||A||M) mod L precomputed (used by
-//                         the generic verify_detached path for mlen != 32).
+//                         signing hash, RippleAddress.cpp:190-200): pre-checks,
+//                         k, decompression of A and R, half-size scalars.
+//   verify_main_kernel    phase 2, the hot loop: [e]B + [c](-A) + [d](-Q) == O,
+//                         accept bits assembled per wave with a 64-bit ballot.
+//   verify_fallback_kernel  full-length check for the rare flagged lanes.
 //   hram_var_kernel       k for arbitrary-length messages.
 //   tx_hash_kernel        SHA512Half(signing preimage) per transaction
 //                         (Serializer.cpp:354-360 / SerializedObject.cpp:444-450).
 //   sign_kernel           RFC 8032 keypair + signature (synthetic data only).
 //
-// Launch geometry: 256-thread workgroups (4 waves), grid sized by the host to
-// the resident capacity and grid-striding over 256-signature tiles, so the
-// per-lane [k](-A) table workspace is bounded by the resident lanes.
+// Launch geometry: 256-thread workgroups (4 waves); phases 2 and 3 use a grid
+// sized by the host to the resident capacity and grid-stride over
+// 256-signature tiles, so the per-lane table workspace is bounded by the
+// resident lanes.
 #include "stl_base_table.h"
 #include "stl_kernels.h"
 #include "stl_verify_core.h"
@@ -21,7 +23,10 @@
 // Occupancy target of the verify kernel (waves per SIMD); register budget =
 // 512 / waves.  Tuned on MI355X ("occupancy").
 #ifndef STL_VERIFY_WAVES_PER_SIMD
-#define STL_VERIFY_WAVES_PER_SIMD 3
+#define STL_VERIFY_WAVES_PER_SIMD 2
+#endif
+#ifndef STL_PRE_WAVES_PER_SIMD
+#define STL_PRE_WAVES_PER_SIMD 2
 #endif
 
 namespace stl {
@@ -39,69 +44,45 @@ __device__ __forceinline__ void st8(uint8_t* p, const uint32_t w[8]) {
   q[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
-// Copy the 128-entry affine base table (14 KiB) into LDS once per workgroup.
-__device__ __forceinline__ void stage_base_table(uint32_t* sB) {
-  const uint32_t* g = &kBaseNiels[0][0];
-  for (uint32_t i = threadIdx.x; i < (uint32_t)(kBaseTableEntries * kBaseNielsWords); i += kBlock) sB[i] = g[i];
+// Copy `tables` affine base tables (14 KiB each) into LDS once per workgroup.
+__device__ __forceinline__ void stage_base_table(uint32_t* sB, int tables) {
+  const uint4* g = reinterpret_cast<const uint4*>(&kBaseNiels[0][0][0]);
+  uint4* d = reinterpret_cast<uint4*>(sB);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(tables * kBaseTableWords / 4); i += kBlock) d[i] = g[i];
   __syncthreads();
 }
 
-__device__ __forceinline__ TableView lane_table(uint4* ws) {
+// Per-lane workspace slot: kSlotQuads uint4 = two 9-entry cached tables,
+// contiguous per lane (one lookup touches 2-3 whole 128-B lines of its own lane).
+__device__ __forceinline__ uint4* lane_slot(uint4* ws) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  // per-lane contiguous entries: one lookup touches 2-3 whole 128-B lines of
-  // its own lane instead of 16 B of nine lines shared by lanes with other digits
-  return TableView{ws + (((size_t)blockIdx.x * (kBlock / 64) + wave) * 64 + lane) * kTableQuads, 1};
+  return ws + (((size_t)blockIdx.x * (kBlock / 64) + wave) * 64 + lane) * kSlotQuads;
 }
 
-__device__ __forceinline__ void ld_pre(PreState& p, const uint4* q) {
-  uint32_t w[28];
+template <int NQ, typename T>
+__device__ __forceinline__ void ld_words(T& out, const uint4* q) {
+  static_assert(sizeof(T) == NQ * 16, "size");
+  uint32_t* w = reinterpret_cast<uint32_t*>(&out);
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
+  for (int i = 0; i < NQ; ++i) {
     const uint4 v = q[i];
     w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
   }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) p.k[i] = w[i];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    p.negAx.v[i] = w[8 + i];
-    p.negAy.v[i] = w[17 + i];
-  }
-  p.ok = w[26];
-  p.pad = 0;
 }
 
-__device__ __forceinline__ void st_pre(uint4* q, const PreState& p) {
-  uint32_t w[28];
+template <int NQ, typename T>
+__device__ __forceinline__ void st_words(uint4* q, const T& in) {
+  static_assert(sizeof(T) == NQ * 16, "size");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&in);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = p.k[i];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    w[8 + i] = p.negAx.v[i];
-    w[17 + i] = p.negAy.v[i];
-  }
-  w[26] = p.ok;
-  w[27] = 0;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  for (int i = 0; i < NQ; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
-// Phase 1: one signature per lane -- pre-checks, k = SHA-512(R||A||M) mod L
-// (or k given, PRE_K), decompression of A.  Signatures [base, base+cnt).
-template <bool PRE_K>
-__global__ __launch_bounds__(kBlock) void verify_pre_kernel(const uint8_t* __restrict__ sig,
-                                                            const uint8_t* __restrict__ msg_or_k,
-                                                            const uint8_t* __restrict__ pk, uint32_t base,
-                                                            uint32_t cnt, uint32_t policy, uint4* __restrict__ pre) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t >= cnt) return;
-  const size_t j = (size_t)base + t;
-  uint32_t R[8], S[8], A[8], M[8], k[8];
-  ld8(R, sig + 64 * j);
-  ld8(S, sig + 64 * j + 32);
-  ld8(A, pk + 32 * j);
+__device__ __forceinline__ void load_k(uint32_t k[8], const uint32_t R[8], const uint32_t A[8],
+                                       const uint8_t* msg_or_k, size_t j, bool pre_k) {
+  uint32_t M[8];
   ld8(M, msg_or_k + 32 * j);
-  if (PRE_K) {
+  if (pre_k) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) k[i] = M[i];
   } else {
@@ -109,36 +90,86 @@ __global__ __launch_bounds__(kBlock) void verify_pre_kernel(const uint8_t* __res
     sha512_hram32(h, R, A, M);
     sc_reduce64(k, h);
   }
-  PreState p;
-  verify_phase1(p, R, S, A, k, policy);
-  st_pre(pre + (size_t)t * 7, p);
 }
 
-// Phase 2: the Straus loop, encode and compare; grid-strides over 256-signature
+// Phase 1: one signature per lane -- pre-checks, k = SHA-512(R||A||M) mod L
+// (or k given, PRE_K), decompression of A and R, lattice reduction of k to
+// half-size (c, d), e = d*S mod L.  Signatures [base, base+cnt); one ballot
+// word of "needs the full-length path" flags per wave.
+template <bool PRE_K>
+__global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_pre_kernel(const uint8_t* __restrict__ sig,
+                                                            const uint8_t* __restrict__ msg_or_k,
+                                                            const uint8_t* __restrict__ pk, uint32_t base,
+                                                            uint32_t cnt, uint32_t policy, uint4* __restrict__ pre,
+                                                            uint64_t* __restrict__ fb_words) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = t < cnt;
+  const size_t j = (size_t)base + (live ? t : cnt - 1);
+  uint32_t R[8], S[8], A[8], k[8];
+  ld8(R, sig + 64 * j);
+  ld8(S, sig + 64 * j + 32);
+  ld8(A, pk + 32 * j);
+  load_k(k, R, A, msg_or_k, j, PRE_K);
+  HalfState h;
+  verify_phase1_half(h, R, S, A, k, policy & 1u);
+  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  if (live) st_words<14>(pre + (size_t)t * 14, h);
+  const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
+  if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
+}
+
+// Phase 2: [e]B + [c](-A) + [d](-Q) == O; grid-strides over 256-signature
 // tiles of [base, base+cnt) so the per-lane table workspace is bounded by the
 // resident lanes; one ballot word per wave.
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_kernel(
-    const uint8_t* __restrict__ sig, const uint4* __restrict__ pre, uint32_t base, uint32_t cnt,
-    uint64_t* __restrict__ bitmap, uint4* __restrict__ ws) {
-  __shared__ uint32_t sB[kBaseTableEntries * kBaseNielsWords];
-  stage_base_table(sB);
-  const TableView tv = lane_table(ws);
+    const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
+    uint4* __restrict__ ws) {
+  __shared__ uint32_t sB[2 * kBaseTableWords];
+  stage_base_table(sB, 2);
+  uint4* slot = lane_slot(ws);
+  const TableView tab1{slot, 1}, tab2{slot + kTableQuads, 1};
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
     const uint32_t t = tile + threadIdx.x;
     const bool live = t < cnt;
-    const uint32_t tt = live ? t : (cnt - 1);  // tail lanes re-read a valid element
-    const size_t j = (size_t)base + tt;
-    PreState p;
-    ld_pre(p, pre + (size_t)tt * 7);
-    uint32_t R[8], S[8];
-    ld8(R, sig + 64 * j);
-    ld8(S, sig + 64 * j + 32);
-    bool ok = verify_phase2(p, R, S, tv, sB);
-    ok = ok && live;
+    HalfState h;
+    ld_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
+    const bool ok = verify_phase2_half(h, tab1, tab2, sB) && live;
     const uint64_t word = __ballot(ok);
     const uint32_t wbase = tile + wave * 64;
     if (lane == 0 && wbase < cnt) bitmap[(base + wbase) >> 6] = word;
+  }
+}
+
+// Full-length path for the lanes phase 1 flagged (rare: the lattice
+// reduction did not fit 2^131).  Waves with no flagged lane skip their tile;
+// flagged lanes OR their exact bit into the word phase 2 wrote.
+template <bool PRE_K>
+__global__ __launch_bounds__(kBlock, 2) void verify_fallback_kernel(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
+    uint32_t base, uint32_t cnt, uint32_t policy, const uint64_t* __restrict__ fb_words,
+    uint64_t* __restrict__ bitmap, uint4* __restrict__ ws) {
+  __shared__ uint32_t sB[kBaseTableWords];
+  stage_base_table(sB, 1);
+  const TableView tab{lane_slot(ws), 1};
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
+    const uint32_t wbase = tile + wave * 64;
+    if (wbase >= cnt) continue;
+    const uint64_t fb = fb_words[wbase >> 6];
+    if (fb == 0) continue;  // wave-uniform
+    bool ok = false;
+    if ((fb >> lane) & 1u) {
+      const size_t j = (size_t)base + wbase + lane;
+      uint32_t R[8], S[8], A[8], k[8];
+      ld8(R, sig + 64 * j);
+      ld8(S, sig + 64 * j + 32);
+      ld8(A, pk + 32 * j);
+      load_k(k, R, A, msg_or_k, j, PRE_K);
+      ok = verify_full_with_k(R, S, A, k, policy & 1u, tab, sB);
+    }
+    const uint64_t word = __ballot(ok);
+    if (lane == 0) bitmap[(base + wbase) >> 6] |= word;
   }
 }
 
@@ -190,9 +221,9 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
                                                       const uint8_t* __restrict__ msg, uint32_t n,
                                                       uint8_t* __restrict__ pk_out, uint8_t* __restrict__ sig_out,
                                                       uint4* __restrict__ ws) {
-  __shared__ uint32_t sB[kBaseTableEntries * kBaseNielsWords];
-  stage_base_table(sB);
-  const TableView tv = lane_table(ws);
+  __shared__ uint32_t sB[kBaseTableWords];
+  stage_base_table(sB, 1);
+  const TableView tv{lane_slot(ws), 1};
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     const uint32_t i = base + threadIdx.x;
     const bool live = i < n;
@@ -248,21 +279,28 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
                          hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  // ws = [per-lane tables: grid x kWsBytesPerBlock][PreState x kPreChunk]
-  uint4* tables = ws;
+  // ws = [per-lane slots: grid x kWsBytesPerBlock][HalfState x kPreChunk][fallback words]
+  uint4* slots = ws;
   uint4* pre = ws + (size_t)grid * (kWsBytesPerBlock / 16);
+  uint64_t* fb = reinterpret_cast<uint64_t*>(pre + (size_t)kPreChunk * 14);
   for (uint32_t base = 0; base < n; base += kPreChunk) {
     const uint32_t cnt = n - base < kPreChunk ? n - base : kPreChunk;
     const dim3 g1((cnt + kBlock - 1) / kBlock);
+    const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
+    const dim3 g2(tiles < grid ? tiles : grid);
     if (pre_k)
       hipLaunchKernelGGL(verify_pre_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
-                         pre);
+                         pre, fb);
     else
       hipLaunchKernelGGL(verify_pre_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                         policy, pre);
-    const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(verify_main_kernel, dim3(tiles < grid ? tiles : grid), dim3(kBlock), 0, stream, sig, pre,
-                       base, cnt, bitmap, tables);
+                         policy, pre, fb);
+    hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots);
+    if (pre_k)
+      hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
+                         policy, fb, bitmap, slots);
+    else
+      hipLaunchKernelGGL(verify_fallback_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
+                         policy, fb, bitmap, slots);
   }
   return hipGetLastError();
 }

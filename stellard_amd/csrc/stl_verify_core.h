@@ -19,7 +19,9 @@
 #pragma once
 #include "stl_ge25519.h"
 #include "stl_sc25519.h"
+#include "stl_lattice.h"
 #include "stl_sha512.h"
+#include "stl_base_table.h"
 
 namespace stl {
 
@@ -128,23 +130,17 @@ STL_HD void load_base_niels(ge_niels& n, const uint32_t* tab, int absd) {
   fe_cmov(n.xy2d, n.xy2d, id.xy2d, z);
 }
 
-// R' = [k](-A) + [S]B  with k, S < 2^253.  negA is the decompressed -A.
-// Joint Straus over 64 nibble positions (shared doublings): k in signed
-// radix 16 (an A-add at every position, 9-entry per-lane table), S in signed
-// radix 256 (a B-add at every even position, 128-entry shared table
-// `btab`, LDS on the device).
-STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8], const uint32_t S[8],
-                              const TableView& tab, const uint32_t* btab) {
-  // ---- table of e*(-A), e = 0..8 ----
+// Per-lane table of cached multiples e*P, e = 0..8 (entry 0 = identity).
+STL_HD void build_cached_table(const TableView& tab, const ge_p3& P) {
   ge_cached c1, c;
   ge_cached_0(c);
   tab.store(0, c);
-  ge_p3_to_cached(c1, negA);
+  ge_p3_to_cached(c1, P);
   tab.store(1, c1);
   ge_p1p1 t;
   ge_p2 p2;
   ge_p3 p3;
-  ge_p3_to_p2(p2, negA);
+  ge_p3_to_p2(p2, P);
   ge_p2_dbl(t, p2);
   ge_p1p1_to_p3(p3, t);
   ge_p3_to_cached(c, p3);
@@ -156,6 +152,46 @@ STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8]
     ge_p3_to_cached(c, p3);
     tab.store(e, c);
   }
+}
+
+// acc + sign(digit) * tab[|digit|], |digit| <= 8
+STL_HD void add_table_digit(ge_p1p1& t, const ge_p3& acc, const TableView& tab, int digit) {
+  ge_cached c;
+  const int a = digit < 0 ? -digit : digit;
+  tab.load(a > 8 ? 8 : a, c);
+  ge_cached_cneg(c, digit < 0);
+  ge_add_cached(t, acc, c);
+}
+
+// acc + sign(digit) * btab[|digit|] (affine base table), |digit| <= 128
+STL_HD void madd_base_digit(ge_p1p1& t, const ge_p3& acc, const uint32_t* btab, int digit) {
+  const int a = digit < 0 ? -digit : digit;
+  ge_niels n;
+  load_base_niels(n, btab, a > 128 ? 128 : a);
+  ge_niels_cneg(n, digit < 0);
+  ge_madd(t, acc, n);
+}
+
+// acc <- [16] acc2: three p2 doublings and a fourth into p3 (for an add)
+STL_HD void dbl4(ge_p3& acc, ge_p2& acc2) {
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int r = 0; r < 3; ++r) {
+    ge_p2_dbl(t, acc2);
+    ge_p1p1_to_p2(acc2, t);
+  }
+  ge_p2_dbl(t, acc2);
+  ge_p1p1_to_p3(acc, t);
+}
+
+// R' = [k](-A) + [S]B  with k, S < 2^253.  negA is the decompressed -A.
+// Joint Straus over 64 nibble positions (shared doublings): k in signed
+// radix 16 (an A-add at every position, 9-entry per-lane table), S in signed
+// radix 256 (a B-add at every even position, 128-entry shared table
+// `btab`, LDS on the device).
+STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8], const uint32_t S[8],
+                              const TableView& tab, const uint32_t* btab) {
+  build_cached_table(tab, negA);
   // ---- signed digits ----
   uint32_t kd[8], sd[8];
   sc_recode16(kd, k);
@@ -177,34 +213,18 @@ STL_HD void double_scalarmult(ge_p2& out, const ge_p3& negA, const uint32_t k[8]
 #pragma unroll
       for (int m = 7; m > 0; --m) sd[m] = sd[m - 1];
     }
-    if (i != 63) {
-#pragma unroll 1
-      for (int r = 0; r < 3; ++r) {
-        ge_p2_dbl(t, acc2);
-        ge_p1p1_to_p2(acc2, t);
-      }
-      ge_p2_dbl(t, acc2);
-      ge_p1p1_to_p3(acc, t);
-    }
+    if (i != 63) dbl4(acc, acc2);
     // A digit (every position)
-    const int da = (int32_t)wa >> 28;
+    ge_p1p1 t;
+    add_table_digit(t, acc, tab, (int32_t)wa >> 28);
     wa <<= 4;
-    const int ada = da < 0 ? -da : da;
-    tab.load(ada > 8 ? 8 : ada, c);
-    ge_cached_cneg(c, da < 0);
-    ge_add_cached(t, acc, c);
     if (i & 1) {
       ge_p1p1_to_p2(acc2, t);
     } else {
       // B digit (even positions: bits 4i .. 4i+7)
       ge_p1p1_to_p3(acc, t);
-      const int db = (int32_t)wb >> 24;
+      madd_base_digit(t, acc, btab, (int32_t)wb >> 24);
       wb <<= 8;
-      const int adb = db < 0 ? -db : db;
-      ge_niels n;
-      load_base_niels(n, btab, adb > 128 ? 128 : adb);
-      ge_niels_cneg(n, db < 0);
-      ge_madd(t, acc, n);
       ge_p1p1_to_p2(acc2, t);
     }
   }
@@ -263,21 +283,192 @@ STL_HD bool verify_phase2(const PreState& p, const uint32_t R[8], const uint32_t
   return p.ok != 0 && eq;
 }
 
-// Full check for one signature given k = H(R||A||M) mod L (8 words).
-STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
-                          uint32_t policy, const TableView& tab, const uint32_t* bniels) {
+// Full-length check given k = H(R||A||M) mod L (8 words): exact for every
+// input; the fallback of the half-size path below.
+STL_HD bool verify_full_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
+                               uint32_t policy, const TableView& tab, const uint32_t* bniels) {
   PreState p;
   verify_phase1(p, R, S, A, k, policy);
   return verify_phase2(p, R, S, tab, bniels);
 }
 
+// ---- half-size-scalar path (stl_lattice.h): [e]B + [c](-A) + [d](-Q) == O ----
+// Phase-1 output, 224 bytes (14 x uint4):
+//   cdig/ddig  signed radix-16 digits 0..39 of |c|, |d| (4-bit packed)
+//   tops       bits 0-7: positions needed (max over c, d; 33 for almost
+//              every lane), bit 16 ok (pre-checks, decodings, S < L),
+//              bit 17 fallback (full-length path)
+//   edig       signed radix-256 digits of e = d*S mod L (32 digits)
+//   P1, P2     affine P1 = sign(c) ? A : -A,  P2 = sign(d) ? Q : -Q
+struct HalfState {
+  uint32_t cdig[5], ddig[5];
+  uint32_t tops;
+  uint32_t edig[8];
+  fe P1x, P1y, P2x, P2y;
+  uint32_t pad;
+};
+static_assert(sizeof(HalfState) == 224, "HalfState must be 14 x uint4");
+constexpr uint32_t kHalfOk = 1u << 16;
+constexpr uint32_t kHalfFallback = 1u << 17;
+
+// encode(P) == R is possible for some point P iff R is a canonical encoding:
+// y < p, and not "x == 0 with the sign bit set" (x == 0 <=> y == +-1).
+STL_HD bool r_is_canonical(const uint32_t R[8]) {
+  if (!point_is_canonical(R)) return false;
+  const bool sign = (R[7] >> 31) != 0;
+  bool one = R[0] == 1u, pm1 = R[0] == 0xffffffecu;
+#pragma unroll
+  for (int i = 1; i < 7; ++i) {
+    one = one && R[i] == 0u;
+    pm1 = pm1 && R[i] == 0xffffffffu;
+  }
+  one = one && (R[7] & 0x7fffffffu) == 0u;
+  pm1 = pm1 && (R[7] & 0x7fffffffu) == 0x7fffffffu;
+  return !(sign && (one || pm1));
+}
+
+STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
+                               const uint32_t k[8], uint32_t policy) {
+  bool ok = verify_prechecks(R, S, A, policy);
+  // stellard composite: && signatureIsCanonical (S < L), RippleAddress.cpp:198-199
+  ok = ok && sc_lt_L(S);
+  ge_p3 negA, negQ;
+  ok = ge_frombytes_negate_vartime(negA, A) && ok;
+  ok = ge_frombytes_negate_vartime(negQ, R) && ok;
+  ok = ok && r_is_canonical(R);
+  uint32_t c[5], d[5];
+  bool c_neg = false, d_neg = false;
+  const bool half = lattice_half(c, c_neg, d, d_neg, k);
+  uint32_t e[8];
+  sc_mul_signed(e, d, d_neg, S);
+  fe nx;
+  fe_neg(nx, negA.X);
+  fe_cmov(o.P1x, negA.X, nx, c_neg);
+  o.P1y = negA.Y;
+  fe_neg(nx, negQ.X);
+  fe_cmov(o.P2x, negQ.X, nx, d_neg);
+  o.P2y = negQ.Y;
+  const int cneed = sc_recode16_half(o.cdig, c);
+  const int dneed = sc_recode16_half(o.ddig, d);
+  sc_recode256(o.edig, e);
+  const int need = cneed > dneed ? cneed : dneed;
+  o.tops = (uint32_t)need | (ok ? kHalfOk : 0u) | (ok && !half ? kHalfFallback : 0u);
+  o.pad = 0;
+}
+
+STL_HD void affine_to_p3(ge_p3& P, const fe& x, const fe& y) {
+  P.X = x;
+  P.Y = y;
+  fe_1(P.Z);
+  fe_mul(P.T, x, y);
+}
+
+// Positions the Straus loop must run for this wave: the largest need of its
+// lanes (wave-uniform; 33 for almost every wave).  `need` in [1, 40].
+STL_HD int half_positions(int need) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int p = 32;
+#pragma unroll
+  for (int b = 33; b <= kHalfDigits; ++b) p = __any(need >= b) ? b : p;
+  return p;
+#else
+  return need > 32 ? need : 32;
+#endif
+}
+
+// [|c|]P1 + [|d|]P2 + [e]B == O ?  Joint Straus over P <= 40 nibble
+// positions (P wave-uniform): c, d in signed radix 16 (9-entry per-lane
+// tables), e in signed radix 256 with its low 16 digits on table 0 (j*B) and
+// high 16 on table 1 (j*2^128*B), both added at even positions i <= 30.
+STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const TableView& tab2,
+                               const uint32_t* btab) {
+  {
+    ge_p3 P;
+    affine_to_p3(P, p.P1x, p.P1y);
+    build_cached_table(tab1, P);
+    affine_to_p3(P, p.P2x, p.P2y);
+    build_cached_table(tab2, P);
+  }
+  const int npos = half_positions((int)(p.tops & 0xffu));
+  uint32_t cd[5], dd[5], ed[8];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    cd[i] = p.cdig[i];
+    dd[i] = p.ddig[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ed[i] = p.edig[i];
+  ge_p3 acc;
+  ge_p2 acc2;
+  ge_p1p1 t;
+  ge_p3_0(acc);
+  ge_p2_0(acc2);
+  uint32_t wc = 0, wd = 0, we0 = 0, we1 = 0;
+#pragma unroll 1
+  for (int i = kHalfDigits - 1; i >= 0; --i) {
+    if ((i & 7) == 7) {  // next 8 radix-16 digits of |c| and |d|
+      wc = cd[4];
+      wd = dd[4];
+#pragma unroll
+      for (int m = 4; m > 0; --m) {
+        cd[m] = cd[m - 1];
+        dd[m] = dd[m - 1];
+      }
+    }
+    if ((i & 7) == 6 && i < 32) {  // next 4 radix-256 digits of e, low and high halves
+      we0 = ed[3];
+      we1 = ed[7];
+#pragma unroll
+      for (int m = 3; m > 0; --m) {
+        ed[m] = ed[m - 1];
+        ed[4 + m] = ed[4 + m - 1];
+      }
+    }
+    const int dc = (int32_t)wc >> 28, dq = (int32_t)wd >> 28;
+    wc <<= 4;
+    wd <<= 4;
+    if (i >= npos) continue;  // wave-uniform: digits above every lane's need are 0
+    if (i != npos - 1) dbl4(acc, acc2);
+    add_table_digit(t, acc, tab1, dc);
+    ge_p1p1_to_p3(acc, t);
+    add_table_digit(t, acc, tab2, dq);
+    if ((i & 1) || i > 31) {
+      ge_p1p1_to_p2(acc2, t);
+    } else {
+      ge_p1p1_to_p3(acc, t);
+      madd_base_digit(t, acc, btab, (int32_t)we0 >> 24);
+      we0 <<= 8;
+      ge_p1p1_to_p3(acc, t);
+      madd_base_digit(t, acc, btab + kBaseTableWords, (int32_t)we1 >> 24);
+      we1 <<= 8;
+      ge_p1p1_to_p2(acc2, t);
+    }
+  }
+  // identity: X == 0 and Y == Z
+  fe ymz;
+  fe_sub(ymz, acc2.Y, acc2.Z);
+  const bool id = fe_iszero(acc2.X) && fe_iszero(ymz);
+  return (p.tops & kHalfOk) != 0 && (p.tops & kHalfFallback) == 0 && id;
+}
+
+// Full check for one signature given k = H(R||A||M) mod L: the half-size path,
+// or the full-length path for the rare lanes whose lattice reduction does not
+// fit.  tab1/tab2 are two per-lane 9-entry tables; btab the two base tables.
+STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
+                          uint32_t policy, const TableView& tab1, const TableView& tab2, const uint32_t* btab) {
+  HalfState h;
+  verify_phase1_half(h, R, S, A, k, policy);
+  if (h.tops & kHalfFallback) return verify_full_with_k(R, S, A, k, policy, tab1, btab);
+  return verify_phase2_half(h, tab1, tab2, btab);
+}
+
 // Fixed 32-byte message (the stellard signing hash): k computed in-lane.
 STL_HD bool verify_msg32(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t M[8],
-                         uint32_t policy, const TableView& tab, const uint32_t* bniels) {
+                         uint32_t policy, const TableView& tab1, const TableView& tab2, const uint32_t* btab) {
   uint32_t h[16], k[8];
   sha512_hram32(h, R, A, M);
   sc_reduce64(k, h);
-  return verify_with_k(R, S, A, k, policy, tab, bniels);
+  return verify_with_k(R, S, A, k, policy, tab1, tab2, btab);
 }
 
 }  // namespace stl

@@ -21,6 +21,8 @@ from . import _native as N
 
 POLICY_SODIUM_1_0_18 = N.STL_POLICY_SODIUM_1_0_18
 POLICY_STELLARD_1_0_0 = N.STL_POLICY_STELLARD_1_0_0
+# OR into `policy` to check with full-length scalars (same bits, slower)
+FULL_LENGTH = N.STL_FULL_LENGTH
 
 
 class BadInputs(RuntimeError):

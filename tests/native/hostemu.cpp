@@ -39,20 +39,68 @@ static void load8(uint32_t w[8], const uint8_t* p) { std::memcpy(w, p, 32); }
 extern "C" {
 
 // Bitmap out, LSB-first; returns number of bound violations observed.
-uint64_t hostemu_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
-                              uint8_t* bitmap, uint32_t policy) {
-  std::vector<uint4> table(81);
-  stl::TableView tv{table.data(), 1};
+// mode 0: the product's path (half-size scalars, full-length fallback);
+// mode 1: full-length path only; mode 2: half-size path only (flagged lanes
+// reject).  Returns the number of limb-bound violations observed; *fallbacks
+// (if non-null) receives the number of lanes the half-size path flagged.
+uint64_t hostemu_verify_batch_mode(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
+                                   uint8_t* bitmap, uint32_t policy, int mode, uint64_t* fallbacks) {
+  std::vector<uint4> table(2 * 81);
+  stl::TableView t1{table.data(), 1}, t2{table.data() + 81, 1};
+  const uint32_t* btab = &stl::kBaseNielsHost[0][0][0];
   std::memset(bitmap, 0, (n + 7) / 8);
+  uint64_t fb = 0;
   for (size_t i = 0; i < n; ++i) {
-    uint32_t R[8], S[8], A[8], M[8];
+    uint32_t R[8], S[8], A[8], M[8], h[16], k[8];
     load8(R, sig + 64 * i);
     load8(S, sig + 64 * i + 32);
     load8(A, pk + 32 * i);
     load8(M, msg + 32 * i);
-    if (stl::verify_msg32(R, S, A, M, policy, tv, &stl::kBaseNielsHost[0][0])) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+    stl::sha512_hram32(h, R, A, M);
+    stl::sc_reduce64(k, h);
+    bool ok;
+    if (mode == 1) {
+      ok = stl::verify_full_with_k(R, S, A, k, policy, t1, btab);
+    } else {
+      stl::HalfState hs;
+      stl::verify_phase1_half(hs, R, S, A, k, policy);
+      const bool flagged = (hs.tops & stl::kHalfFallback) != 0;
+      fb += flagged;
+      if (flagged && mode == 0) ok = stl::verify_full_with_k(R, S, A, k, policy, t1, btab);
+      else ok = stl::verify_phase2_half(hs, t1, t2, btab);
+    }
+    if (ok) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
   }
+  if (fallbacks) *fallbacks = fb;
   return g_bound_viol.load();
+}
+
+uint64_t hostemu_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
+                              uint8_t* bitmap, uint32_t policy) {
+  return hostemu_verify_batch_mode(sig, msg, pk, n, bitmap, policy, 0, nullptr);
+}
+
+// Lattice reduction of k (32 bytes LE) to (c, d): magnitudes as 20-byte LE
+// integers, signs in *signs (bit 0 c < 0, bit 1 d < 0).  Returns 1 if the pair
+// fits the half-size budget, 0 if the lane takes the full-length path.
+int hostemu_lattice(const uint8_t kb[32], uint8_t c_out[20], uint8_t d_out[20], uint32_t* signs) {
+  uint32_t k[8], c[5], d[5];
+  load8(k, kb);
+  bool cn = false, dn = false;
+  const bool ok = stl::lattice_half(c, cn, d, dn, k);
+  std::memcpy(c_out, c, 20);
+  std::memcpy(d_out, d, 20);
+  *signs = (cn ? 1u : 0u) | (dn ? 2u : 0u);
+  return ok ? 1 : 0;
+}
+
+// e = d * S mod L with signed d (20-byte magnitude, sign), S 32 bytes.
+void hostemu_sc_mul_signed(const uint8_t d_in[20], int d_neg, const uint8_t S_in[32], uint8_t out[32]) {
+  uint32_t d[5], S[8], o[8];
+  std::memcpy(d, d_in, 20);
+  load8(S, S_in);
+  stl::sc_mul_signed(o, d, d_neg != 0, S);
+  std::memcpy(out, o, 32);
 }
 
 uint64_t hostemu_bound_checks(void) { return g_bound_checks.load(); }

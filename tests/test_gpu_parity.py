@@ -226,3 +226,40 @@ def test_tx_verify_batch_vs_oracle(stl, oracle):
     got = stl.tx_verify_batch(pre, sig, pk)
     assert np.array_equal(got, exp)
     assert 0.5 < exp.mean() < 0.9
+
+
+@pytest.mark.parametrize("policy", [0, 1])
+def test_full_length_flag_same_bits(stl, golden, oracle, torch_cuda, policy):
+    """STL_FULL_LENGTH routes every lane through the full-length fallback
+    kernel ([S]B - [k]A, 253-bit chain); the default half-size-scalar path
+    must give the same bits, and both the golden / oracle bits."""
+    torch = torch_cuda
+    sig, msg, pk = _golden_arrays(golden)
+    key = "expected_sodium_1_0_18" if policy == 0 else "expected_stellard_1_0_0_unpinned"
+    full = stl.verify_batch(sig, msg, pk, policy=policy | stl.FULL_LENGTH)
+    assert np.array_equal(full, golden[key].astype(bool))
+    n = 4096
+    s2, m2, p2 = _gpu_signed(stl, torch, n, 77 + policy)
+    rng = np.random.default_rng(3 + policy)
+    s2, m2, p2 = _mutate(s2.cpu().numpy(), m2.cpu().numpy(), p2.cpu().numpy(), rng)
+    half = stl.verify_batch(s2, m2, p2, policy=policy)
+    full = stl.verify_batch(s2, m2, p2, policy=policy | stl.FULL_LENGTH)
+    assert np.array_equal(half, full)
+    assert np.array_equal(half, oracle.verify_batch(s2, m2, p2, policy=policy, threads=16))
+
+
+def test_chunk_boundary(stl, oracle, torch_cuda):
+    """n just above the phase-1 chunk (2^20): two chunks, bitmap words of the
+    second chunk land after the first; mutated rows straddle the boundary."""
+    torch = torch_cuda
+    n = (1 << 20) + 4097
+    sig, msg, pk = _gpu_signed(stl, torch, n, 4242)
+    sig = sig.clone()
+    bad_rows = torch.tensor([0, 5, (1 << 20) - 1, 1 << 20, (1 << 20) + 63, (1 << 20) + 64, n - 1], device=sig.device)
+    sig[bad_rows, 33] ^= 1
+    words = stl.verify_batch_device(sig, msg, pk)
+    torch.cuda.synchronize()
+    got = stl.words_to_bool(words, n)
+    exp = np.ones(n, bool)
+    exp[bad_rows.cpu().numpy()] = False
+    assert np.array_equal(got, exp)
