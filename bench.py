@@ -180,6 +180,8 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
                          "kernel_ms": kern_ms, "work_per_verify": W_VERIFY,
+                         "kernels": "verify_pre + verify_main + verify_fallback, one stream, HIP events around "
+                                    "each stl_ed25519_verify_batch_device call",
                          "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9)},
             "cpu_baseline": None,
         }

@@ -36,7 +36,7 @@
 // Scheduling fence after each field multiply: keeps the pre-RA scheduler from
 // software-pipelining consecutive products (which multiplies live registers
 // and forced spills at 2-4 waves/SIMD).  Device-only hint; no-op on the host.
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(STL_NO_FE_FENCE)
 #define STL_FE_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define STL_FE_FENCE()

@@ -118,6 +118,63 @@ LATK(l_lshr64, uint64_t, A_LSHR64)
 LATK(l_lshladd64, uint64_t, A_LSHLADD64)
 LATK(l_add, uint32_t, A_ADD)
 
+// ---- manual two-way interleave of independent field multiplies: each mad is
+// ordered by an empty asm on its accumulator, so the column chains start from
+// their carry-in (no reassociation) and the ILP comes from the partner product.
+#define MADF(acc, x, y)                     \
+  do {                                      \
+    acc += (uint64_t)(x) * (y);             \
+    asm volatile("" : "+v"(acc));           \
+  } while (0)
+
+__device__ __forceinline__ void fe_mul2_manual(stl::fe& h1, const stl::fe& a1, const stl::fe& b1, stl::fe& h2,
+                                               const stl::fe& a2, const stl::fe& b2) {
+  const stl::fe A1 = a1, B1 = b1, A2 = a2, B2 = b2;
+  uint64_t hc1[8], hc2[8];
+#pragma unroll
+  for (int k = 9; k < 17; ++k) {
+    uint64_t c1 = 0, c2 = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int j = k - i;
+      if (j < 0 || j > 8) continue;
+      MADF(c1, A1.v[i], B1.v[j]);
+      MADF(c2, A2.v[i], B2.v[j]);
+    }
+    hc1[k - 9] = c1;
+    hc2[k - 9] = c2;
+  }
+  uint64_t cy1 = 0, cy2 = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    uint64_t c1 = cy1, c2 = cy2;
+    if (k < 8) {
+      MADF(c1, (uint32_t)hc1[k], 1216u);
+      MADF(c2, (uint32_t)hc2[k], 1216u);
+    }
+    if (k > 0) {
+      MADF(c1, (uint32_t)(hc1[k - 1] >> 32), 9728u);
+      MADF(c2, (uint32_t)(hc2[k - 1] >> 32), 9728u);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int j = k - i;
+      if (j < 0 || j > 8) continue;
+      MADF(c1, A1.v[i], B1.v[j]);
+      MADF(c2, A2.v[i], B2.v[j]);
+    }
+    h1.v[k] = (uint32_t)c1 & stl::M29;
+    h2.v[k] = (uint32_t)c2 & stl::M29;
+    cy1 = c1 >> 29;
+    cy2 = c2 >> 29;
+  }
+  uint64_t u1 = (uint64_t)h1.v[0] + cy1 * 1216u, u2 = (uint64_t)h2.v[0] + cy2 * 1216u;
+  h1.v[0] = (uint32_t)u1 & stl::M29;
+  h1.v[1] += (uint32_t)(u1 >> 29);
+  h2.v[0] = (uint32_t)u2 & stl::M29;
+  h2.v[1] += (uint32_t)(u2 >> 29);
+}
+
 // ---- field-operation kernels: two independent chains per lane ----
 #define FE_ITERS 64
 template <int OP>
@@ -125,7 +182,7 @@ __global__ void k_fe(uint64_t* out, uint64_t* cyc, uint32_t a0, uint32_t b0) {
   stl::fe a, b, c, d;
   for (int i = 0; i < 9; ++i) {
     a.v[i] = (threadIdx.x * 2654435761u + i * a0) & stl::M29;
-    b.v[i] = (0x9e3779b9u * (i + b0)) & stl::M29;
+    b.v[i] = (0x9e3779b9u * (i + b0) + threadIdx.x * 77u) & stl::M29;
     c.v[i] = a.v[i] ^ 0x55u;
     d.v[i] = b.v[i] ^ 0x1234u;
   }
@@ -136,6 +193,7 @@ __global__ void k_fe(uint64_t* out, uint64_t* cyc, uint32_t a0, uint32_t b0) {
     if (OP == 0) { stl::fe_mul(a, a, b); stl::fe_mul(c, c, d); }
     if (OP == 1) { stl::fe_sq(a, a); stl::fe_sq(c, c); }
     if (OP == 2) { stl::fe_sub(a, a, b); stl::fe_sub(c, c, d); }
+    if (OP == 3) { fe_mul2_manual(a, a, b, c, c, d); }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   uint32_t x = 0;
@@ -196,7 +254,7 @@ int main() {
     if (run(k.f, cus, 1, ITERS * 16.0, &c1, d, dc)) return 1;
     printf("latency %-18s %8.2f cycles (dependent chain, 1 wave/SIMD)\n", k.name, c1);
   }
-  struct { const char* name; kfn f; } fs[] = {{"fe_mul", k_fe<0>}, {"fe_sq", k_fe<1>}, {"fe_sub", k_fe<2>}};
+  struct { const char* name; kfn f; } fs[] = {{"fe_mul", k_fe<0>}, {"fe_sq", k_fe<1>}, {"fe_sub", k_fe<2>}, {"fe_mul2", k_fe<3>}};
   for (auto& k : fs) {
     printf("%-8s", k.name);
     for (int w = 1; w <= 4; ++w) {

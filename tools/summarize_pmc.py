@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Summarise tools/pmc_ab.sh: per variant, median per-dispatch SQ counters of
-the verify kernel and derived ratios (cycle counters are quad-cycles)."""
+"""Summarise rocprofv3 --pmc passes (tools/pmc_ab.sh): per variant and per
+kernel, median per-dispatch counter values and derived ratios (SQ cycle
+counters are quad-cycles; FETCH_SIZE / WRITE_SIZE are KiB)."""
 import csv
 import glob
 import json
@@ -14,18 +15,23 @@ for path in sorted(glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv
     variant = os.path.relpath(path, d).split(os.sep)[0]
     agg = {}
     for r in csv.DictReader(open(path)):
-        if "verify_kernel" not in r["Kernel_Name"]:
+        kname = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if "verify" not in kname:
             continue
-        key = (r["Dispatch_Id"], r["Counter_Name"])
+        key = (kname, r["Dispatch_Id"], r["Counter_Name"])
         agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
     per = {}
-    for (_, c), v in agg.items():
-        per.setdefault(c, []).append(v)
-    med = {c: statistics.median(v) for c, v in per.items()}
-    wc = med.get("SQ_WAVE_CYCLES", 0) or 1
-    med["frac_wait_any"] = med.get("SQ_WAIT_ANY", 0) / wc
-    med["frac_wait_inst_any"] = med.get("SQ_WAIT_INST_ANY", 0) / wc
-    med["frac_active_inst_any"] = med.get("SQ_ACTIVE_INST_ANY", 0) / wc
-    res[variant] = med
+    for (k, _, c), v in agg.items():
+        per.setdefault(k, {}).setdefault(c, []).append(v)
+    out = {}
+    for k, cs in per.items():
+        med = {c: statistics.median(v) for c, v in cs.items()}
+        wc = med.get("SQ_WAVE_CYCLES", 0)
+        if wc:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in med:
+                    med["frac_" + c[3:].lower()] = med[c] / wc
+        out[k] = med
+    res.setdefault(variant, {}).update(out)
 json.dump(res, open(os.path.join(d, "summary.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))

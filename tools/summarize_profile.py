@@ -1,56 +1,74 @@
 #!/usr/bin/env python3
-"""Summarise a profile_rNN.sh run: per-launch HBM traffic of the verify kernel
-from the PMC passes (FETCH_SIZE/WRITE_SIZE are KiB; reported raw and with the
-gfx950 x2 FETCH correction of MI355X_MICROARCH.md 'HBM' as an upper bound),
-kernel-trace stats, and SQ counters.  Writes <dir>/summary.json."""
+"""Summarise a tools/profile.sh run.  Per verify kernel (pre / main /
+fallback): kernel-trace average duration, FETCH_SIZE / WRITE_SIZE per launch
+(KiB x 1024; FETCH raw and with the gfx950 x2 wide-read correction of
+MI355X_MICROARCH.md 'HBM' as an upper bound) and SQ counters; totals per
+verify launch sequence (one stl_ed25519_verify_batch_device call = the three
+kernels on one stream).  Writes <dir>/summary.json; with --traffic also
+profiles/traffic_latest.json, which bench.py reports as roofline.traffic."""
 import csv
+import glob
 import json
 import os
 import statistics
 import sys
 
 d = sys.argv[1]
-KERNEL = "verify_kernel<false>"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kname(s):
+    return s.split("(")[0].replace("void ", "").strip()
 
 
 def pmc(sub):
-    path = os.path.join(d, sub, "run_counter_collection.csv")
-    if not os.path.exists(path):
-        return {}
-    agg = {}
-    for r in csv.DictReader(open(path)):
-        if KERNEL not in r["Kernel_Name"]:
-            continue
-        key = (r["Dispatch_Id"], r["Counter_Name"])
-        agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
     out = {}
-    for (_, c), v in agg.items():
-        out.setdefault(c, []).append(v)
-    return {c: statistics.median(v) for c, v in out.items()}
+    for path in glob.glob(os.path.join(d, sub, "**", "*counter_collection.csv"), recursive=True):
+        agg = {}
+        for r in csv.DictReader(open(path)):
+            k = kname(r["Kernel_Name"])
+            if "verify" not in k:
+                continue
+            key = (k, r["Dispatch_Id"], r["Counter_Name"])
+            agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
+        for (k, _, c), v in agg.items():
+            out.setdefault(k, {}).setdefault(c, []).append(v)
+    return {k: {c: statistics.median(v) for c, v in cs.items()} for k, cs in out.items()}
 
 
 stats = {}
-sp = os.path.join(d, "trace", "run_kernel_stats.csv")
-if os.path.exists(sp):
-    for r in csv.DictReader(open(sp)):
-        stats[r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                                          "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
-f = pmc("pmc_fetch")
-w = pmc("pmc_write")
-sq = pmc("pmc_sq")
-fetch_b = f.get("FETCH_SIZE", 0.0) * 1024
-write_b = w.get("WRITE_SIZE", 0.0) * 1024
-summary = {
-    "kernel_stats": stats,
-    "fetch_bytes_raw": fetch_b,
-    "write_bytes": write_b,
-    "hbm_bytes_per_launch": fetch_b + write_b,
-    "hbm_bytes_per_launch_fetch_x2_upper": 2 * fetch_b + write_b,
-    "sq": sq,
-}
-if sq.get("GRBM_GUI_ACTIVE") and stats:
-    v = [s for k, s in stats.items() if "verify_kernel" in k]
-    if v:
-        summary["effective_clock_ghz"] = sq["GRBM_GUI_ACTIVE"] / 8 / (v[0]["avg_ns"] * 1e-9) / 1e9
+for path in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
+    for r in csv.DictReader(open(path)):
+        stats[kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                   "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+f, w, sq = pmc("pmc_fetch"), pmc("pmc_write"), pmc("pmc_sq")
+kernels = sorted(set(f) | set(w) | set(sq) | {k for k in stats if "verify" in k})
+per = {}
+tot = {"fetch_bytes_raw": 0.0, "write_bytes": 0.0, "avg_ns": 0.0}
+for k in kernels:
+    fb = f.get(k, {}).get("FETCH_SIZE", 0.0) * 1024
+    wb = w.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+    e = {"fetch_bytes_raw": fb, "write_bytes": wb, "sq": sq.get(k, {}), "trace": stats.get(k)}
+    s = sq.get(k, {})
+    if s.get("GRBM_GUI_ACTIVE") and stats.get(k):
+        e["effective_clock_ghz"] = s["GRBM_GUI_ACTIVE"] / 8 / (stats[k]["avg_ns"] * 1e-9) / 1e9
+    if s.get("SQ_WAVE_CYCLES"):
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            e["frac_" + c[3:].lower()] = s.get(c, 0.0) / s["SQ_WAVE_CYCLES"]
+    per[k] = e
+    tot["fetch_bytes_raw"] += fb
+    tot["write_bytes"] += wb
+    tot["avg_ns"] += stats.get(k, {}).get("avg_ns", 0.0)
+tot["hbm_bytes_per_launch"] = tot["fetch_bytes_raw"] + tot["write_bytes"]
+tot["hbm_bytes_per_launch_fetch_x2_upper"] = 2 * tot["fetch_bytes_raw"] + tot["write_bytes"]
+summary = {"kernels": per, "verify_launch_sequence": tot,
+           "other_kernels": {k: v for k, v in stats.items() if "verify" not in k}}
 json.dump(summary, open(os.path.join(d, "summary.json"), "w"), indent=1)
+if "--traffic" in sys.argv:
+    json.dump({"source": f"{d}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, summed "
+                         "over verify_pre/main/fallback kernels, one verify launch sequence of the bench batch)",
+               "hbm_bytes_per_launch": tot["hbm_bytes_per_launch"],
+               "hbm_bytes_per_launch_fetch_x2_upper": tot["hbm_bytes_per_launch_fetch_x2_upper"],
+               "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, raw; FETCH x2 (gfx950 wide-read correction) upper bound"},
+              open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w"), indent=1)
 print(json.dumps(summary, indent=1))
