@@ -31,6 +31,7 @@
 #ifndef STL_BOUND_MUL
 #define STL_BOUND_MUL(a, b)
 #define STL_BOUND_SUB(a, b)
+#define STL_BOUND_SUBK(a, b, K)
 #endif
 
 // Scheduling fence after each field multiply: keeps the pre-RA scheduler from
@@ -96,85 +97,313 @@ STL_HD void fe_neg(fe& h, const fe& a) {
   fe_carry(h);
 }
 
+// Lazy (carry-free) forms.  fe_sub_nc<K>: h = a + K*Z1 - b, no carry pass;
+// requires every limb of b <= the matching limb of K*Z1 (alpha_b < K) and
+// alpha_a + K < 8 (no 32-bit overflow); output alpha <= alpha_a + K.  Used
+// where the consumer is a multiply whose alpha product stays <= 7
+// (bounds annotated at each call site in stl_ge25519.h).
+template <int K>
+STL_HD void fe_sub_nc(fe& h, const fe& a, const fe& b) {
+  STL_BOUND_SUBK(a, b, K);
+  h.v[0] = a.v[0] + (uint32_t)K * 0x1ffffb40u - b.v[0];
+#pragma unroll
+  for (int i = 1; i < 9; ++i) h.v[i] = a.v[i] + (uint32_t)K * M29 - b.v[i];
+}
+
+// h = K*Z1 - a, no carry pass (alpha_a < K); output alpha <= K.
+template <int K>
+STL_HD void fe_neg_nc(fe& h, const fe& a) {
+  fe z;
+  fe_0(z);
+  fe_sub_nc<K>(h, z, a);
+}
+
 // h = c ? b : a  (lane-wise select, no branch)
 STL_HD void fe_cmov(fe& h, const fe& a, const fe& b, bool c) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) h.v[i] = c ? b.v[i] : a.v[i];
 }
 
-// Product-scanning reduction shared by fe_mul / fe_sq.  COL(k, init) yields
-// init + the 64-bit sum of the partial products of column k (k = 0..16, each
-// sum < 63 * 2^58).  Fold by register halves: the high columns 9..16 are kept as raw 64-bit sums
-// and folded into the low columns by their 32-bit register halves (no 29-bit
-// normalisation chain for them): the low half of column k+9 enters column k
-// with weight 2^261 == 1216, the high half enters column k+1 with weight
-// 2^(261+32-29) == 1216*8 = 9728.  Each low column then starts its mad chain
-// from (carry + the two fold terms), so a column costs its products plus one
-// and + one 64-bit shift.  Bound: column sums <= 63*2^58*(1+2^-12) plus the
-// fold terms < 2^46 stay below 2^64.  Measured on MI355X against the earlier
-// schedule that normalised columns 9..16 to 29-bit digits first (one and, one
-// 64-bit shift and one 64-bit add per column): 98 vs 91 mads but 22 vs 57 other
-// instructions per multiply; verify kernel 14.09 -> 13.31 ms per 1M.
-#define STL_FE_REDUCE_COLUMNS(h, COL)                                    \
-  do {                                                                  \
-    uint64_t hc_[8];                                                    \
-    _Pragma("unroll") for (int k = 9; k < 17; ++k) hc_[k - 9] = COL(k, 0ull); \
-    uint64_t carry_ = 0;                                                \
-    _Pragma("unroll") for (int k = 0; k < 9; ++k) {                     \
-      uint64_t init_ = carry_;                                          \
-      if (k < 8) init_ += (uint64_t)(uint32_t)hc_[k < 8 ? k : 0] * 1216u; \
-      if (k > 0) init_ += (uint64_t)(uint32_t)(hc_[k > 0 ? k - 1 : 0] >> 32) * 9728u; \
-      const uint64_t t_ = COL(k, init_);                                \
-      (h).v[k] = (uint32_t)t_ & M29;                                    \
-      carry_ = t_ >> 29;                                                \
-    }                                                                   \
-    /* carry_ < 2^35 has weight 2^261 == 1216 */                        \
-    const uint64_t u_ = (uint64_t)(h).v[0] + carry_ * 1216u;            \
-    (h).v[0] = (uint32_t)u_ & M29;                                      \
-    (h).v[1] += (uint32_t)(u_ >> 29);                                   \
-  } while (0)
+// ---- multiplication -------------------------------------------------------
+// Products are scheduled by hand for gfx950: a fixed order that overlaps
+// independent v_mad_u64_u32 chains:
+//
+//   * every column is one mad chain that STARTS from its carry-in / fold
+//     terms (no 64-bit re-association add at the end of the chain, which the
+//     compiler otherwise inserts to shorten the critical path);
+//   * the high column k+11 (a chain from zero) runs alongside low column k;
+//   * NOPS independent products (two squarings of a doubling, two products
+//     of an addition) are interleaved mad by mad, so each wave always has 2-4
+//     independent chains in flight -- a wave issues a mad64 only every ~9
+//     cycles (tools/microbench/isarate.hip) and a SIMD holds two waves.
+//
+// The order is pinned by an empty asm on each accumulator after each mad
+// (madf / STL_ACC_FENCE); the compiler still allocates registers and schedules every
+// other instruction.  On the host the fence is a no-op and the result is the
+// same integer arithmetic.
+//
+// Reduction ("fold by halves"): the high columns 9..16 are kept as raw 64-bit
+// sums and folded into the low columns by their 32-bit register halves: the
+// low half of column k+9 enters column k with weight 2^261 == 1216, the high
+// half enters column k+1 with weight 2^(261+32-29) == 9728.  Bound: column
+// sums <= 63*2^58*(1+2^-12) plus the fold terms < 2^46 stay below 2^64.
+// Measured on MI355X (tools/microbench/isarate.hip, SIMD cycles per product
+// at 2 waves/SIMD): the compiler-scheduled fold 580 (mul) / 457 (sq); this
+// schedule 569 / 442 alone and 545 / 408 per product when two are paired.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define STL_ACC_FENCE(acc) asm volatile("" : "+v"(acc))
+#else
+#define STL_ACC_FENCE(acc)
+#endif
 
-
-STL_HD uint64_t fe_mul_col(const fe& a, const fe& b, int k, uint64_t acc) {
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int j = k - i;
-    if (j < 0 || j > 8) continue;
-    acc += (uint64_t)a.v[i] * b.v[j];
-  }
-  return acc;
+// One multiply-accumulate term of a column chain.
+STL_HD void madf(uint64_t& acc, uint32_t x, uint32_t y) {
+  acc += (uint64_t)x * y;
+  STL_ACC_FENCE(acc);
 }
 
-// d = 2a (precomputed); column k of a^2 = sum_{i<j} d_i a_j + [k even] a_{k/2}^2
-STL_HD uint64_t fe_sq_col(const fe& a, const uint32_t d[9], int k, uint64_t acc) {
-  if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int j = k - i;
-    if (j <= i || j > 8) continue;
-    acc += (uint64_t)d[i] * a.v[j];
-  }
-  return acc;
+// Operands of one product: a*b (SQ = false) or a^2 with d = 2a (SQ = true).
+template <bool SQ>
+struct ProdSrc {
+  uint32_t a[9], b[9];  // b = a (SQ: b holds d = 2a)
+};
+
+// Number of terms of column k, and term t = (x, y) of column k.
+template <bool SQ>
+STL_HD constexpr int col_terms(int k) {
+  const int lo = k > 8 ? k - 8 : 0;
+  if (!SQ) return (k < 8 ? k : 8) - lo + 1;
+  const int pairs = k >= 1 ? (k - 1) / 2 - lo + 1 : 0;  // i < j, i + j = k
+  return (pairs > 0 ? pairs : 0) + ((k & 1) == 0 ? 1 : 0);
 }
 
-STL_HD void fe_mul(fe& h, const fe& a, const fe& b) {
-  STL_BOUND_MUL(a, b);
-  const fe a_ = a, b_ = b;  // h may alias a or b
-#define STL_MUL_COL(k, init) fe_mul_col(a_, b_, (k), (init))
-  STL_FE_REDUCE_COLUMNS(h, STL_MUL_COL);
-#undef STL_MUL_COL
+template <bool SQ>
+STL_HD void col_term(const ProdSrc<SQ>& s, int k, int t, uint32_t& x, uint32_t& y) {
+  const int lo = k > 8 ? k - 8 : 0;
+  if (!SQ) {
+    const int i = lo + t;
+    x = s.a[i];
+    y = s.b[k - i];
+  } else if ((k & 1) == 0 && t == 0) {
+    x = s.a[k >> 1];
+    y = s.a[k >> 1];
+  } else {
+    const int i = lo + t - ((k & 1) == 0 ? 1 : 0);
+    x = s.b[i];  // 2 a_i
+    y = s.a[k - i];
+  }
+}
+
+// Run up to eight column chains (chain c: product c % NOPS, column kcol[c];
+// kcol < 0 = none) round-robin, term by term, accumulating into acc[c].
+template <bool SQ, int NOPS>
+STL_HD void run_cols(const ProdSrc<SQ>* src, uint64_t* acc, const int* kcol, int nch) {
+  int len[8], mx = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    len[c] = (c < nch && kcol[c] >= 0) ? col_terms<SQ>(kcol[c]) : 0;
+    mx = len[c] > mx ? len[c] : mx;
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    if (t >= mx) break;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (c >= nch || t >= len[c]) continue;
+      uint32_t x, y;
+      col_term<SQ>(src[c % NOPS], kcol[c], t, x, y);
+      madf(acc[c], x, y);
+    }
+  }
+}
+
+// h[j] = product j (mod p), j < NOPS <= 4, alpha <= 1 + 2^-12 (as fe_mul /
+// fe_sq; same input bounds).  Phase P0 runs columns 9 and 10 of every
+// product; phase Pk (k = 0..8) runs low column k alongside high column k+11
+// (k <= 5).  Low column k starts from carry, then lo(col k+9)*1216 and
+// hi(col k+8)*9728 (2^261 == 1216, 2^(261+3) == 9728 mod p).
+template <bool SQ, int NOPS>
+STL_HD void fe_prod_n(fe* h, const ProdSrc<SQ>* src) {
+  uint64_t hc[NOPS][8];  // high columns 9..16 (about four live at a time)
+  {
+    uint64_t acc[8];
+    int kc[8];
+#pragma unroll
+    for (int c = 0; c < 2 * NOPS; ++c) {
+      acc[c] = 0;
+      kc[c] = 9 + c / NOPS;
+    }
+    run_cols<SQ, NOPS>(src, acc, kc, 2 * NOPS);
+#pragma unroll
+    for (int c = 0; c < 2 * NOPS; ++c) hc[c % NOPS][c / NOPS] = acc[c];
+  }
+  uint64_t carry[NOPS];
+#pragma unroll
+  for (int j = 0; j < NOPS; ++j) carry[j] = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    uint64_t acc[8];
+    int kc[8];
+    const bool hi = k + 11 <= 16;
+#pragma unroll
+    for (int j = 0; j < NOPS; ++j) {
+      acc[j] = carry[j];
+      kc[j] = k;
+      acc[NOPS + j] = 0;
+      kc[NOPS + j] = hi ? k + 11 : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < NOPS; ++j)
+      if (k < 8) madf(acc[j], (uint32_t)hc[j][k], 1216u);
+#pragma unroll
+    for (int j = 0; j < NOPS; ++j)
+      if (k > 0) madf(acc[j], (uint32_t)(hc[j][k - 1] >> 32), 9728u);
+    run_cols<SQ, NOPS>(src, acc, kc, hi ? 2 * NOPS : NOPS);
+#pragma unroll
+    for (int j = 0; j < NOPS; ++j) {
+      h[j].v[k] = (uint32_t)acc[j] & M29;
+      carry[j] = acc[j] >> 29;
+      if (hi) hc[j][k + 2] = acc[NOPS + j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NOPS; ++j) {
+    const uint64_t u = (uint64_t)h[j].v[0] + carry[j] * 1216u;
+    h[j].v[0] = (uint32_t)u & M29;
+    h[j].v[1] += (uint32_t)(u >> 29);
+  }
+}
+
+// Entry points: one product (fe_mul, fe_sq) or two interleaved (fe_mul2, fe_sq2).
+STL_HD void fe_mul2(fe& h0, const fe& a0, const fe& b0, fe& h1, const fe& a1, const fe& b1) {
+  STL_BOUND_MUL(a0, b0);
+  STL_BOUND_MUL(a1, b1);
+  ProdSrc<false> s[2];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    s[0].a[i] = a0.v[i];
+    s[0].b[i] = b0.v[i];
+    s[1].a[i] = a1.v[i];
+    s[1].b[i] = b1.v[i];
+  }
+  fe h[2];
+  fe_prod_n<false, 2>(h, s);
+  h0 = h[0];
+  h1 = h[1];
   STL_FE_FENCE();
 }
 
-STL_HD void fe_sq(fe& h, const fe& a) {
-  STL_BOUND_MUL(a, a);
-  const fe a_ = a;
-  uint32_t d[9];
+STL_HD void fe_sq2(fe& h0, const fe& a0, fe& h1, const fe& a1) {
+  STL_BOUND_MUL(a0, a0);
+  STL_BOUND_MUL(a1, a1);
+  ProdSrc<true> s[2];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) d[i] = a_.v[i] << 1;  // alpha <= 2.64 => fits 32 bits
-#define STL_SQ_COL(k, init) fe_sq_col(a_, d, (k), (init))
-  STL_FE_REDUCE_COLUMNS(h, STL_SQ_COL);
-#undef STL_SQ_COL
+  for (int i = 0; i < 9; ++i) {
+    s[0].a[i] = a0.v[i];
+    s[0].b[i] = a0.v[i] << 1;
+    s[1].a[i] = a1.v[i];
+    s[1].b[i] = a1.v[i] << 1;
+  }
+  fe h[2];
+  fe_prod_n<true, 2>(h, s);
+  h0 = h[0];
+  h1 = h[1];
+  STL_FE_FENCE();
+}
+
+// N independent products interleaved (N <= 4): with three or four chains in
+// flight a dependent mad is always >= 3 instructions after its predecessor,
+// so no hazard s_nop is needed and each wave keeps 3-4 mads in flight.
+template <int N>
+STL_HD void fe_mul_n(fe* h, const fe* const* a, const fe* const* b) {
+  ProdSrc<false> s[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    STL_BOUND_MUL(*a[j], *b[j]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      s[j].a[i] = a[j]->v[i];
+      s[j].b[i] = b[j]->v[i];
+    }
+  }
+  fe_prod_n<false, N>(h, s);
+  STL_FE_FENCE();
+}
+
+template <int N>
+STL_HD void fe_sq_n(fe* h, const fe* const* a) {
+  ProdSrc<true> s[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    STL_BOUND_MUL(*a[j], *a[j]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      s[j].a[i] = a[j]->v[i];
+      s[j].b[i] = a[j]->v[i] << 1;
+    }
+  }
+  fe_prod_n<true, N>(h, s);
+  STL_FE_FENCE();
+}
+
+STL_HD void fe_mul3(fe& h0, const fe& a0, const fe& b0, fe& h1, const fe& a1, const fe& b1, fe& h2, const fe& a2,
+                    const fe& b2) {
+  const fe* a[3] = {&a0, &a1, &a2};
+  const fe* b[3] = {&b0, &b1, &b2};
+  fe h[3];
+  fe_mul_n<3>(h, a, b);
+  h0 = h[0];
+  h1 = h[1];
+  h2 = h[2];
+}
+
+STL_HD void fe_mul4(fe& h0, const fe& a0, const fe& b0, fe& h1, const fe& a1, const fe& b1, fe& h2, const fe& a2,
+                    const fe& b2, fe& h3, const fe& a3, const fe& b3) {
+  const fe* a[4] = {&a0, &a1, &a2, &a3};
+  const fe* b[4] = {&b0, &b1, &b2, &b3};
+  fe h[4];
+  fe_mul_n<4>(h, a, b);
+  h0 = h[0];
+  h1 = h[1];
+  h2 = h[2];
+  h3 = h[3];
+}
+
+STL_HD void fe_sq4(fe& h0, const fe& a0, fe& h1, const fe& a1, fe& h2, const fe& a2, fe& h3, const fe& a3) {
+  const fe* a[4] = {&a0, &a1, &a2, &a3};
+  fe h[4];
+  fe_sq_n<4>(h, a);
+  h0 = h[0];
+  h1 = h[1];
+  h2 = h[2];
+  h3 = h[3];
+}
+
+STL_HD void fe_mul(fe& h0, const fe& a0, const fe& b0) {
+  STL_BOUND_MUL(a0, b0);
+  ProdSrc<false> s[1];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    s[0].a[i] = a0.v[i];
+    s[0].b[i] = b0.v[i];
+  }
+  fe h[1];
+  fe_prod_n<false, 1>(h, s);
+  h0 = h[0];
+  STL_FE_FENCE();
+}
+
+STL_HD void fe_sq(fe& h0, const fe& a0) {
+  STL_BOUND_MUL(a0, a0);
+  ProdSrc<true> s[1];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    s[0].a[i] = a0.v[i];
+    s[0].b[i] = a0.v[i] << 1;
+  }
+  fe h[1];
+  fe_prod_n<true, 1>(h, s);
+  h0 = h[0];
   STL_FE_FENCE();
 }
 

@@ -333,9 +333,9 @@ STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t
   // stellard composite: && signatureIsCanonical (S < L), RippleAddress.cpp:198-199
   ok = ok && sc_lt_L(S);
   ge_p3 negA, negQ;
-  ok = ge_frombytes_negate_vartime(negA, A) && ok;
-  ok = ge_frombytes_negate_vartime(negQ, R) && ok;
-  ok = ok && r_is_canonical(R);
+  bool okA, okR;
+  ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
+  ok = ok && okA && okR && r_is_canonical(R);
   uint32_t c[5], d[5];
   bool c_neg = false, d_neg = false;
   const bool half = lattice_half(c, c_neg, d, d_neg, k);
@@ -428,10 +428,18 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     wc <<= 4;
     wd <<= 4;
     if (i >= npos) continue;  // wave-uniform: digits above every lane's need are 0
+    // Issue this position's two table loads ahead of the doublings (~15k
+    // cycles of independent work per wave): their latency (L2 / Infinity
+    // Cache) is hidden instead of stalling the adds.
+    ge_cached ca, cq;
+    tab1.load(dc < 0 ? -dc : dc, ca);
+    tab2.load(dq < 0 ? -dq : dq, cq);
     if (i != npos - 1) dbl4(acc, acc2);
-    add_table_digit(t, acc, tab1, dc);
+    ge_cached_cneg(ca, dc < 0);
+    ge_add_cached(t, acc, ca);
     ge_p1p1_to_p3(acc, t);
-    add_table_digit(t, acc, tab2, dq);
+    ge_cached_cneg(cq, dq < 0);
+    ge_add_cached(t, acc, cq);
     if ((i & 1) || i > 31) {
       ge_p1p1_to_p2(acc2, t);
     } else {

@@ -13,9 +13,11 @@ static std::atomic<uint64_t> g_bound_checks{0};
 
 #define STL_BOUND_MUL(a, b) hostemu_check_mul((a), (b))
 #define STL_BOUND_SUB(a, b) hostemu_check_sub((a), (b))
+#define STL_BOUND_SUBK(a, b, K) hostemu_check_subk((a), (b), (K))
 namespace stl { struct fe; }
 static void hostemu_check_mul(const stl::fe& a, const stl::fe& b);
 static void hostemu_check_sub(const stl::fe& a, const stl::fe& b);
+static void hostemu_check_subk(const stl::fe& a, const stl::fe& b, int k);
 
 #include "../../stellard_amd/csrc/stl_base_table.h"
 #include "../../stellard_amd/csrc/stl_verify_core.h"
@@ -28,6 +30,14 @@ static double alpha(const stl::fe& a) {
 static void hostemu_check_mul(const stl::fe& a, const stl::fe& b) {
   g_bound_checks++;
   if (alpha(a) * alpha(b) > 7.0) g_bound_viol++;
+}
+// fe_sub_nc<K>: no limb of b above K*Z1's, and a + K*Z1 within 32 bits
+static void hostemu_check_subk(const stl::fe& a, const stl::fe& b, int k) {
+  g_bound_checks++;
+  bool bad = b.v[0] > (uint64_t)k * 0x1ffffb40u;
+  for (int i = 1; i < 9; ++i) bad = bad || b.v[i] > (uint64_t)k * 0x1fffffffu;
+  for (int i = 0; i < 9; ++i) bad = bad || (uint64_t)a.v[i] + (uint64_t)k * 0x1fffffffu > 0xffffffffull;
+  if (bad) g_bound_viol++;
 }
 static void hostemu_check_sub(const stl::fe& a, const stl::fe& b) {
   g_bound_checks++;

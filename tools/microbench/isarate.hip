@@ -194,6 +194,10 @@ __global__ void k_fe(uint64_t* out, uint64_t* cyc, uint32_t a0, uint32_t b0) {
     if (OP == 1) { stl::fe_sq(a, a); stl::fe_sq(c, c); }
     if (OP == 2) { stl::fe_sub(a, a, b); stl::fe_sub(c, c, d); }
     if (OP == 3) { fe_mul2_manual(a, a, b, c, c, d); }
+    if (OP == 4) { stl::fe_mul2(a, a, b, c, c, d); }
+    if (OP == 5) { stl::fe_mul(a, a, b); stl::fe_mul(c, c, d); }
+    if (OP == 6) { stl::fe_sq2(a, a, c, c); }
+    if (OP == 7) { stl::fe_sq(a, a); stl::fe_sq(c, c); }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   uint32_t x = 0;
@@ -254,7 +258,8 @@ int main() {
     if (run(k.f, cus, 1, ITERS * 16.0, &c1, d, dc)) return 1;
     printf("latency %-18s %8.2f cycles (dependent chain, 1 wave/SIMD)\n", k.name, c1);
   }
-  struct { const char* name; kfn f; } fs[] = {{"fe_mul", k_fe<0>}, {"fe_sq", k_fe<1>}, {"fe_sub", k_fe<2>}, {"fe_mul2", k_fe<3>}};
+  struct { const char* name; kfn f; } fs[] = {{"fe_mul", k_fe<0>}, {"fe_sq", k_fe<1>}, {"fe_sub", k_fe<2>}, {"fe_mul2", k_fe<3>}, {"mul2_n", k_fe<4>}, {"mul1_n", k_fe<5>},
+                                        {"sq2_n", k_fe<6>}, {"sq1_n", k_fe<7>}};
   for (auto& k : fs) {
     printf("%-8s", k.name);
     for (int w = 1; w <= 4; ++w) {
