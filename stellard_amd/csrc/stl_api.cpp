@@ -54,8 +54,9 @@ struct Device {
   uint32_t grid = 0;  // resident workgroups for the verify kernel
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf ws, sig, msg, pk, bitmap, pre, off, len;
-  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;  // device-resident API
+  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr;
+  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
+  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;  // tx-hash work counter
   std::mutex ws_mu;
 };
 
@@ -101,6 +102,20 @@ int stream_workspace(Device& d, hipStream_t s, uint4** ws) {
   return STL_OK;
 }
 
+// One-word work counter for (device, stream) of the device-resident tx hash.
+int stream_counter(Device& d, hipStream_t s, uint32_t** ctr) {
+  std::lock_guard<std::mutex> lk(d.ws_mu);
+  auto& slot = d.stream_ctr[s];
+  if (!slot) slot.reset(new DevBuf());
+  int rc = slot->ensure(256);
+  if (rc) return rc;
+  *ctr = static_cast<uint32_t*>(slot->p);
+  return STL_OK;
+}
+
+// tx-hash grid: 8 workgroups per CU (the kernel pulls preimages from a counter)
+uint32_t hash_grid(const Device& d) { return (uint32_t)d.cus * 8u; }
+
 uint32_t grid_for(const Device& d, size_t n) {
   const size_t tiles = (n + stl::kBlock - 1) / stl::kBlock;
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(tiles, d.grid));
@@ -143,12 +158,15 @@ int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t
       end = std::max<uint64_t>(end, off[lo + i] + len[lo + i]);
     }
     const size_t bytes = (size_t)(end - base);
-    if ((rc = d.pre.ensure(bytes ? bytes : 1)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4))) return rc;
+    if ((rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
+        (rc = d.ctr.ensure(256)))
+      return rc;
     if (bytes) STL_TRY(hipMemcpyAsync(d.pre.p, pre + base, bytes, hipMemcpyHostToDevice, s));
     STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, s));
     STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, s));
     STL_TRY(stl::launch_tx_hash(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p),
-                                static_cast<uint32_t*>(d.len.p), (uint32_t)n, static_cast<uint8_t*>(d.msg.p), s));
+                                static_cast<uint32_t*>(d.len.p), (uint32_t)n, static_cast<uint8_t*>(d.msg.p),
+                                static_cast<uint32_t*>(d.ctr.p), hash_grid(d), s));
   }
   STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                              static_cast<uint8_t*>(d.pk.p), (uint32_t)n, static_cast<uint64_t*>(d.bitmap.p), policy,
@@ -234,8 +252,9 @@ void stl_shutdown(void) {
     std::lock_guard<std::mutex> dl(d->mu);
     (void)hipSetDevice(d->ordinal);
     (void)hipStreamSynchronize(d->stream);
-    for (DevBuf* b : {&d->ws, &d->sig, &d->msg, &d->pk, &d->bitmap, &d->pre, &d->off, &d->len}) b->release();
+    for (DevBuf* b : {&d->ws, &d->sig, &d->msg, &d->pk, &d->bitmap, &d->pre, &d->off, &d->len, &d->ctr}) b->release();
     for (auto& kv : d->stream_ws) kv.second->release();
+    for (auto& kv : d->stream_ctr) kv.second->release();
     (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();
@@ -332,7 +351,13 @@ int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offse
   if (!d_preimages || !d_offset || !d_len || !d_msg || n > 0xffffffc0ull) return STL_EINVAL;
   int rc = ensure_init();
   if (rc) return rc;
-  STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, static_cast<hipStream_t>(stream)));
+  const int di = current_device_index();
+  if (di < 0) return STL_ENODEV;
+  Device& d = *g_devs[di];
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* ctr = nullptr;
+  if ((rc = stream_counter(d, s, &ctr))) return rc;
+  STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(d), s));
   return STL_OK;
 }
 

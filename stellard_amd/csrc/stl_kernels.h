@@ -30,8 +30,10 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
                          hipStream_t stream);
 hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t* m, const uint64_t* moff,
                            const uint64_t* mlen, uint32_t n, uint8_t* k_out, hipStream_t stream);
+// counter: one device word of scratch (reset by the launcher); grid: upper
+// bound on workgroups (the kernel pulls work from the counter)
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          hipStream_t stream);
+                          uint32_t* counter, uint32_t grid, hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
                        uint32_t grid, hipStream_t stream);
 

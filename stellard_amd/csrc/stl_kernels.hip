@@ -192,16 +192,58 @@ __global__ void hram_var_kernel(const uint8_t* __restrict__ sig, const uint8_t* 
   st8(k_out + 32 * (size_t)i, k);
 }
 
-// msg_i = SHA512Half(preimage_i)
-__global__ void tx_hash_kernel(const uint8_t* __restrict__ pre, const uint64_t* __restrict__ off,
-                               const uint32_t* __restrict__ len, uint32_t n, uint8_t* __restrict__ msg) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// msg_i = SHA512Half(preimage_i) (Serializer.cpp:354-360 via
+// STObject::getSigningHash, SerializedObject.cpp:444-450).  Lanes pull
+// preimages from a global counter and advance one 128-byte block per
+// iteration, refilling as they finish: waves stay full whatever the length
+// mix (config 5: 100 B - 4 KB, log-uniform), with no sort pass.
+__global__ __launch_bounds__(kBlock) void tx_hash_kernel(const uint8_t* __restrict__ pre,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ len, uint32_t n,
+                                                         uint8_t* __restrict__ msg, uint32_t* __restrict__ counter) {
+  const uint32_t lane = threadIdx.x & 63u;
+  ByteStream bs;
+  bs.init(pre, 0);
   uint64_t st[8];
-  sha512_prefixed(st, nullptr, 0, pre + off[i], len[i]);
-  uint32_t h[16];
-  sha512_digest_le32(h, st);
-  st8(msg + 32 * (size_t)i, h);
+  sha512_init(st);
+  uint32_t mi = 0, blk = 0, nb = 0;
+  bool active = false, exhausted = false;
+  for (;;) {
+    const uint64_t need = __ballot(!active);
+    if (need != 0 && !exhausted) {  // wave-uniform
+      const int leader = __ffsll((unsigned long long)need) - 1;
+      uint32_t base = 0;
+      if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(need));
+      base = __shfl(base, leader);
+      exhausted = base + (uint32_t)__popcll(need) >= n;
+      if (!active) {
+        mi = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+        if (mi < n) {
+          bs.init(pre + off[mi], len[mi]);
+          nb = bs.blocks();
+          blk = 0;
+          sha512_init(st);
+          active = true;
+        }
+      }
+    }
+    if (!__any(active)) break;
+    if (active) {
+      uint64_t w[16];
+      bs.block(w, blk, blk + 1 == nb);
+      sha512_compress(st, w);
+      if (++blk == nb) {
+        uint32_t h[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          h[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+          h[2 * j + 1] = bswap32((uint32_t)st[j]);
+        }
+        st8(msg + 32 * (size_t)mi, h);
+        active = false;
+      }
+    }
+  }
 }
 
 // SHA-512 of a short word-aligned input (nwords even, nwords*4 <= 108 bytes).
@@ -313,9 +355,13 @@ hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t*
 }
 
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          hipStream_t stream) {
+                          uint32_t* counter, uint32_t grid, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(tx_hash_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, pre, off, len, n, msg);
+  hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(tx_hash_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, pre, off, len, n,
+                     msg, counter);
   return hipGetLastError();
 }
 

@@ -144,6 +144,91 @@ STL_HD void sha512_prefixed(uint64_t st[8], const uint8_t* prefix, uint32_t plen
   }
 }
 
+// ---- word-granular streaming SHA-512 over a byte string at any alignment ----
+// The transaction path (SHA512Half of the signing preimage, config 5: 100 B to
+// 4 KB) reads each 128-byte block as 33 aligned dwords and shifts them into
+// message order with v_alignbyte_b32 (one load per 4 bytes instead of one per
+// byte).  The 3 bytes of the last aligned dword past the message are never
+// read: that dword is assembled from byte loads.
+
+STL_HD uint32_t align_byte(uint32_t hi, uint32_t lo, uint32_t shift) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbyte(hi, lo, shift);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (shift & 3)));
+#endif
+}
+
+// Message view: bytes [p, p + len).  q = p rounded down to 4, mis = p & 3,
+// nw = aligned dwords holding message bytes.
+struct ByteStream {
+  const uint8_t* p;
+  const uint32_t* q;
+  uint32_t mis, len, nw;
+  STL_HD void init(const uint8_t* ptr, uint32_t n) {
+    p = ptr;
+    mis = (uint32_t)((uintptr_t)ptr & 3u);
+    q = reinterpret_cast<const uint32_t*>(ptr - mis);
+    len = n;
+    nw = (mis + n + 3) >> 2;
+  }
+  // aligned dword idx of q[] (0 past the message; the last one byte by byte)
+  STL_HD uint32_t dword(uint32_t idx) const {
+    if (idx + 1 < nw || (idx + 1 == nw && ((mis + len) & 3u) == 0)) return q[idx];
+    if (idx + 1 != nw) return 0u;
+    const uint32_t valid = (mis + len) & 3u;  // bytes of the last dword inside the message
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(q + idx);
+    uint32_t v = 0;
+    for (uint32_t t = 0; t < valid; ++t) v |= (uint32_t)b[t] << (8 * t);
+    return v;
+  }
+  // block blk as 16 big-endian words with the FIPS 180-4 padding applied
+  // (0x80 after the message, zeros, 128-bit length in the final block)
+  STL_HD void block(uint64_t w[16], uint32_t blk, bool last) const {
+    uint32_t prev = dword(32 * blk);
+#pragma unroll
+    for (int j = 0; j < 32; j += 2) {
+      uint32_t m[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t next = dword(32 * blk + j + h + 1);
+        uint32_t v = align_byte(next, prev, mis);
+        prev = next;
+        const int64_t keep = (int64_t)len - (int64_t)(128 * blk + 4 * (j + h));
+        if (keep < 4) {
+          v = keep <= 0 ? 0u : (v & ((1u << (8 * keep)) - 1u));
+          if (keep >= 0) v |= 0x80u << (8 * keep);
+        }
+        m[h] = v;
+      }
+      w[j >> 1] = be64_from_le32(m[0], m[1]);
+    }
+    if (last) {
+      w[14] = 0;
+      w[15] = (uint64_t)len * 8;
+    }
+  }
+  STL_HD uint32_t blocks() const { return (len + 17 + 127) / 128; }
+};
+
+// SHA512Half(bytes) -> 8 little-endian words (the first 32 digest bytes)
+STL_HD void sha512_half_words(uint32_t out[8], const uint8_t* p, uint32_t len) {
+  ByteStream bs;
+  bs.init(p, len);
+  uint64_t st[8], w[16];
+  sha512_init(st);
+  const uint32_t nb = bs.blocks();
+  for (uint32_t b = 0; b < nb; ++b) {
+    bs.block(w, b, b + 1 == nb);
+    sha512_compress(st, w);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+    out[2 * j + 1] = bswap32((uint32_t)st[j]);
+  }
+}
+
 STL_HD void sha512_digest_le32(uint32_t out[16], const uint64_t st[8]) {
   for (int j = 0; j < 8; ++j) {
     out[2 * j] = bswap32((uint32_t)(st[j] >> 32));

@@ -104,6 +104,13 @@ int hostemu_lattice(const uint8_t kb[32], uint8_t c_out[20], uint8_t d_out[20], 
   return ok ? 1 : 0;
 }
 
+// SHA512Half over bytes [p, p + len) with the kernel's word-granular reader.
+void hostemu_sha512_half(const uint8_t* p, uint32_t len, uint8_t out[32]) {
+  uint32_t o[8];
+  stl::sha512_half_words(o, p, len);
+  std::memcpy(out, o, 32);
+}
+
 // e = d * S mod L with signed d (20-byte magnitude, sign), S 32 bytes.
 void hostemu_sc_mul_signed(const uint8_t d_in[20], int d_neg, const uint8_t S_in[32], uint8_t out[32]) {
   uint32_t d[5], S[8], o[8];

@@ -131,4 +131,5 @@ def load_hostemu():
     lib.hostemu_lattice.restype = ctypes.c_int
     lib.hostemu_lattice.argtypes = [V, V, V, V]
     lib.hostemu_sc_mul_signed.argtypes = [V, ctypes.c_int, V, V]
+    lib.hostemu_sha512_half.argtypes = [V, ctypes.c_uint32, V]
     return lib

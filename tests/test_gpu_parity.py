@@ -263,3 +263,32 @@ def test_chunk_boundary(stl, oracle, torch_cuda):
     exp = np.ones(n, bool)
     exp[bad_rows.cpu().numpy()] = False
     assert np.array_equal(got, exp)
+
+
+def test_tx_hash_device_config5(stl, torch_cuda):
+    """SHA512Half over 20,000 preimages of log-uniform length 100 B - 4 KB at
+    arbitrary byte offsets (config 5 shape), device entry point, against
+    hashlib; lanes of one wave see very different block counts (work queue)."""
+    import ctypes
+
+    from stellard_amd import _native as N
+    torch = torch_cuda
+    rng = np.random.default_rng(31)
+    n = 20000
+    lens = np.exp(rng.uniform(np.log(100), np.log(4096), n)).astype(np.uint32)
+    gaps = rng.integers(0, 7, n).astype(np.uint64)  # odd alignments
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    total = int(offs[-1] + lens[-1])
+    blob = rng.integers(0, 256, total, dtype=np.uint8)
+    d_blob, d_off, d_len = (torch.from_numpy(a).cuda() for a in (blob, offs.view(np.int64), lens.view(np.int32)))
+    d_msg = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    N.check(N.load().stl_tx_hash_batch_device(ctypes.c_void_p(d_blob.data_ptr()), ctypes.c_void_p(d_off.data_ptr()),
+                                              ctypes.c_void_p(d_len.data_ptr()), n, ctypes.c_void_p(d_msg.data_ptr()),
+                                              ctypes.c_void_p(s.cuda_stream)), "stl_tx_hash_batch_device")
+    torch.cuda.synchronize()
+    got = d_msg.cpu().numpy()
+    for i in range(n):
+        o, ln = int(offs[i]), int(lens[i])
+        assert got[i].tobytes() == hashlib.sha512(blob[o:o + ln].tobytes()).digest()[:32], i
