@@ -99,6 +99,76 @@ def tx_verify_batch(preimages, sig, pk, policy=POLICY_SODIUM_1_0_18):
     return unpack_bitmap(bitmap, n)
 
 
+# ---- transaction level: SerializedTransaction::checkSign ----
+
+class SignedTx:
+    """The signature-check state of one SerializedTransaction.
+
+    Mirrors src/ripple_app/misc/SerializedTransaction.cpp:192-230 and the
+    cache flags of SerializedTransaction.h:116-131: ``signing_pub_key`` is the
+    sfSigningPubKey VL field (any length), ``txn_signature`` the sfTxnSignature
+    VL field (None when absent: getFieldVL returns an empty Blob,
+    SerializedObject.cpp:814), ``preimage`` the signing preimage
+    "STX\\0" || fields without TxnSignature (STObject::getSigningHash,
+    SerializedObject.cpp:444-450)."""
+
+    def __init__(self, signing_pub_key, txn_signature, preimage):
+        self.signing_pub_key = bytes(signing_pub_key)
+        self.txn_signature = None if txn_signature is None else bytes(txn_signature)
+        self.preimage = bytes(preimage)
+        self.sig_good = False   # mSigGood
+        self.sig_bad = False    # mSigBad
+
+    def well_formed(self):
+        """verifySignature throws on a key that is not 32 bytes or a signature
+        that is not 64 (RippleAddress.cpp:192-194); checkSign maps the throw to
+        false (SerializedTransaction.cpp:211-217, 226-229)."""
+        return len(self.signing_pub_key) == 32 and self.txn_signature is not None and len(self.txn_signature) == 64
+
+    def set_good(self):
+        self.sig_good = True
+
+    def check_sign(self, policy=POLICY_SODIUM_1_0_18):
+        """SerializedTransaction::checkSign(): cached verdict, else verify."""
+        return check_sign_batch([self], policy=policy)[0]
+
+
+def check_sign_batch(txs, policy=POLICY_SODIUM_1_0_18, mark="both"):
+    """checkSign over many transactions with one stl_tx_verify_batch call.
+
+    Cached rows return their verdict (mSigGood / mSigBad); malformed rows are
+    rejected on the host and never reach the GPU.  ``mark="both"`` records
+    both verdicts like the serial path; ``mark="good_only"`` records accepts
+    only -- the ledger-close pre-verify, which must
+    not call setBad() because LedgerConsensus.cpp:2101-2106 applies unflagged
+    transactions without a signature check.  Returns a list of bools."""
+    if mark not in ("both", "good_only"):
+        raise ValueError("mark must be 'both' or 'good_only'")
+    out = [False] * len(txs)
+    todo = []
+    for i, t in enumerate(txs):
+        if t.sig_good:
+            out[i] = True
+        elif t.sig_bad:
+            out[i] = False
+        elif not t.well_formed():
+            if mark == "both":
+                t.sig_bad = True
+        else:
+            todo.append(i)
+    if todo:
+        sig = np.frombuffer(b"".join(txs[i].txn_signature for i in todo), np.uint8).reshape(-1, 64)
+        pk = np.frombuffer(b"".join(txs[i].signing_pub_key for i in todo), np.uint8).reshape(-1, 32)
+        bits = tx_verify_batch([txs[i].preimage for i in todo], sig, pk, policy=policy)
+        for i, b in zip(todo, bits):
+            out[i] = bool(b)
+            if b:
+                txs[i].sig_good = True
+            elif mark == "both":
+                txs[i].sig_bad = True
+    return out
+
+
 # ---- device-resident (torch tensors as HBM buffers; torch is plumbing only) ----
 
 def _stream_ptr(stream):

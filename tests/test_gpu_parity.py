@@ -292,3 +292,34 @@ def test_tx_hash_device_config5(stl, torch_cuda):
     for i in range(n):
         o, ln = int(offs[i]), int(lens[i])
         assert got[i].tobytes() == hashlib.sha512(blob[o:o + ln].tobytes()).digest()[:32], i
+
+
+def test_check_sign_batch_mixed(stl, oracle):
+    """SerializedTransaction::checkSign mirror over a mixed batch: well-formed
+    rows through stl_tx_verify_batch (bits == CPU oracle), B12 malformed rows
+    rejected on the host, cache flags set like the serial path."""
+    rng = np.random.default_rng(44)
+    keys = [oracle.keypair(rng.bytes(32)) for _ in range(8)]
+    txs, exp = [], []
+    for i in range(300):
+        pkb, sk = keys[i % 8]
+        pre = b"STX\x00" + rng.bytes(int(rng.integers(100, 600)))
+        s = bytearray(oracle.sign(hashlib.sha512(pre).digest()[:32], sk))
+        kind = i % 6
+        if kind == 1:
+            s[int(rng.integers(64))] ^= 1 << int(rng.integers(8))
+        if kind == 2:
+            txs.append(stl.SignedTx(pkb + b"\x00", bytes(s), pre))
+            exp.append(False)
+            continue
+        if kind == 3:
+            txs.append(stl.SignedTx(pkb, None, pre))
+            exp.append(False)
+            continue
+        txs.append(stl.SignedTx(pkb, bytes(s), pre))
+        sig = np.frombuffer(bytes(s), np.uint8).reshape(1, 64)
+        exp.append(bool(oracle.tx_verify_batch([pre], sig, np.frombuffer(pkb, np.uint8).reshape(1, 32))[0]))
+    got = stl.check_sign_batch(txs)
+    assert got == exp
+    assert all(t.sig_good == e and t.sig_bad == (not e) for t, e in zip(txs, exp))
+    assert stl.check_sign_batch(txs) == exp  # cached verdicts
