@@ -110,6 +110,39 @@ int stl_ed25519_verify_batch_device(const uint8_t *d_sig, const uint8_t *d_msg, 
 int stl_tx_hash_batch_device(const uint8_t *d_preimages, const uint64_t *d_offset, const uint32_t *d_len,
                              size_t n, uint8_t *d_msg, void *stream);
 
+/* ---- serialized transactions ----
+ * checkSign straight from serialized transactions -- the bytes of
+ * TMTransaction.rawTransaction, or what STObject::add writes: n blobs at
+ * blobs[offset[i] .. offset[i]+len[i]), each the full transaction including
+ * its TxnSignature field.  Replaces, per transaction, the
+ * SerializedTransaction(SerializerIterator&) -> getSigningHash ->
+ * checkSign sequence (SerializedTransaction.cpp:65-92,162-165,192-230) and
+ * getTransactionID (SerializedTransaction.cpp:167-171).  The device splices
+ * the signing preimage out of the blob ("STX\0" || blob minus TxnSignature,
+ * Signature, TxnSignatures), which equals the reference's re-serialisation
+ * when the blob is in canonical form; it checks that form and DEFERS every
+ * blob it cannot prove canonical (stellard_amd/csrc/stl_txblob.h lists the
+ * rules).  Blobs are assumed to be transactions the reference constructs
+ * (template checks are the caller's, done when it built the object).
+ * Per-transaction status: */
+#define STL_TX_OK 0        /* accept bit = checkSign(); tx_id valid */
+#define STL_TX_DEFERRED 1  /* accept bit 0; caller runs its own checkSign; tx_id zero */
+#define STL_TX_MALFORMED 2 /* SigningPubKey not 32 B or TxnSignature not 64 B: checkSign()
+                              is false (RippleAddress.cpp:192-194); accept bit 0; tx_id valid */
+
+/* status: n bytes or NULL; tx_id: n*32 bytes (SHA512Half("TXN\0" || blob)) or NULL. */
+int stl_tx_blob_verify_batch(const uint8_t *blobs, const uint64_t *offset, const uint32_t *len, size_t n,
+                             uint8_t *accept_bitmap, uint8_t *status, uint8_t *tx_id, uint32_t flags);
+
+/* Device-resident first half: writes the verify inputs (d_msg n*32, d_sig
+ * n*64, d_pk n*32; a deferred or malformed transaction gets a signature that
+ * always rejects), d_status (n bytes) and, if d_tx_id is not NULL, the
+ * transaction IDs (n*32).  Follow with stl_ed25519_verify_batch_device on the
+ * same stream. */
+int stl_tx_blob_prepare_device(const uint8_t *d_blobs, const uint64_t *d_offset, const uint32_t *d_len,
+                               size_t n, uint8_t *d_msg, uint8_t *d_sig, uint8_t *d_pk, uint8_t *d_tx_id,
+                               uint8_t *d_status, void *stream);
+
 /* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;
  * EdKeyPair::setSeed, EdKeyPair.cpp:25-33): RFC 8032 keypair from a 32-byte
  * seed and a detached signature over a 32-byte message. */

@@ -65,6 +65,29 @@ void oracle_tx_verify_batch(const uint8_t *preimages, const uint64_t *offset,
                             const uint32_t *len, const uint8_t *sig, const uint8_t *pk,
                             size_t n, uint8_t *bitmap, uint32_t policy, int threads);
 
+/* ---- serialized transactions (stl_oracle_tx.c) ----
+ * The reference's deserialise + re-serialise of one transaction blob
+ * (SerializedTransaction(SerializerIterator&), STObject::set/add).
+ * Returns 0 when the blob deserialises (and has a TransactionType, no
+ * duplicate top-level field), -1 where the reference constructor throws.
+ * signing: "STX\0" || add(s, false); full: add(s, true); both up to cap bytes. */
+typedef struct oracle_txinfo {
+  size_t signing_len, full_len;
+  long pk_len, sig_len;      /* top-level SigningPubKey / TxnSignature payload sizes, -1 absent */
+  uint8_t pk[64], sig[64];   /* their first bytes */
+  int max_depth;             /* deepest nesting level reached (top-level fields = 0) */
+  int all_declared;          /* every field code declared in SerializeDeclarations.h */
+  int stopped_early;         /* a top-level 0xE1 ended the parse before the blob end */
+} oracle_txinfo;
+int oracle_tx_blob(const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *full, size_t cap,
+                   oracle_txinfo *info);
+
+/* checkSign over serialized transactions: bit = deserialises && |pk| = 32 &&
+ * |sig| = 64 && verify(SHA512Half(signing)).  tx_id (n*32, may be NULL):
+ * SHA512Half("TXN\0" || full), zero where the blob does not deserialise. */
+void oracle_tx_blob_verify_batch(const uint8_t *blobs, const uint64_t *offset, const uint32_t *len, size_t n,
+                                 uint8_t *bitmap, uint8_t *tx_id, uint32_t policy, int threads);
+
 /* Instrumentation: field multiplications / squarings executed by the last
  * single-threaded oracle_verify call (for the frozen work model). */
 void oracle_op_counts(uint64_t *muls, uint64_t *sqs);

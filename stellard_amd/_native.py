@@ -22,6 +22,11 @@ STL_POLICY_MASK = 0x1
 STL_REQUIRE_S_LT_L = 0x2
 STL_FULL_LENGTH = 0x4
 
+# per-transaction status of the serialized-transaction entry points
+STL_TX_OK = 0
+STL_TX_DEFERRED = 1
+STL_TX_MALFORMED = 2
+
 # Every entry point include/stl.h declares: (name, restype, argtypes)
 _P = ctypes.c_void_p
 _U8P = ctypes.c_void_p
@@ -39,6 +44,10 @@ SYMBOLS = [
      [_U8P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
     ("stl_tx_hash_batch_device", ctypes.c_int, [_U8P, _P, _P, ctypes.c_size_t, _U8P, _P]),
     ("stl_ed25519_sign_batch_device", ctypes.c_int, [_U8P, _U8P, ctypes.c_size_t, _U8P, _U8P, _P]),
+    ("stl_tx_blob_verify_batch", ctypes.c_int,
+     [_U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, ctypes.c_uint32]),
+    ("stl_tx_blob_prepare_device", ctypes.c_int,
+     [_U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, _U8P, _U8P, _P]),
 ]
 
 

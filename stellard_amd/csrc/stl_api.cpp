@@ -54,7 +54,7 @@ struct Device {
   uint32_t grid = 0;  // resident workgroups for the verify kernel
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr;
+  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status;
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;  // tx-hash work counter
   std::mutex ws_mu;
@@ -179,6 +179,51 @@ int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t
   return STL_OK;
 }
 
+// Serialized-transaction shard [lo, hi) on device d: canonical pass, hashes,
+// verify; writes the host bitmap bytes and, when asked, status and tx ids.
+int run_blob_shard(Device& d, const uint8_t* blobs, const uint64_t* off, const uint32_t* len, size_t lo, size_t hi,
+                   uint8_t* bitmap, uint8_t* status, uint8_t* txid, uint32_t policy) {
+  const size_t n = hi - lo;
+  if (n == 0) return STL_OK;
+  std::lock_guard<std::mutex> lk(d.mu);
+  STL_TRY(hipSetDevice(d.ordinal));
+  int rc;
+  const size_t words = (n + 63) / 64;
+  const uint64_t base = off[lo];
+  uint64_t end = base;
+  std::vector<uint64_t> roff(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (off[lo + i] < base) return STL_EINVAL;
+    roff[i] = off[lo + i] - base;
+    end = std::max<uint64_t>(end, off[lo + i] + len[lo + i]);
+  }
+  const size_t bytes = (size_t)(end - base);
+  if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(n * 64)) ||
+      (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)) ||
+      (rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
+      (rc = d.ctr.ensure(256)) || (rc = d.status.ensure(n)) || (txid && (rc = d.txid.ensure(n * 32))))
+    return rc;
+  hipStream_t s = d.stream;
+  if (bytes) STL_TRY(hipMemcpyAsync(d.pre.p, blobs + base, bytes, hipMemcpyHostToDevice, s));
+  STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, s));
+  STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, s));
+  STL_TRY(stl::launch_tx_blob(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p),
+                              static_cast<uint32_t*>(d.len.p), (uint32_t)n, static_cast<uint8_t*>(d.msg.p),
+                              static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.pk.p),
+                              txid ? static_cast<uint8_t*>(d.txid.p) : nullptr, static_cast<uint8_t*>(d.status.p),
+                              static_cast<uint32_t*>(d.ctr.p), hash_grid(d), s));
+  STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
+                             static_cast<uint8_t*>(d.pk.p), (uint32_t)n, static_cast<uint64_t*>(d.bitmap.p), policy,
+                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false, s));
+  std::vector<uint8_t> host_words(words * 8);
+  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
+  if (status) STL_TRY(hipMemcpyAsync(status + lo, d.status.p, n, hipMemcpyDeviceToHost, s));
+  if (txid) STL_TRY(hipMemcpyAsync(txid + 32 * lo, d.txid.p, n * 32, hipMemcpyDeviceToHost, s));
+  STL_TRY(hipStreamSynchronize(s));
+  std::memcpy(bitmap + lo / 8, host_words.data(), (n + 7) / 8);
+  return STL_OK;
+}
+
 int run_batch(const uint8_t* sig, const uint8_t* msg32, const uint8_t* pk, const uint8_t* pre, const uint64_t* off,
               const uint32_t* len, size_t n, uint8_t* bitmap, uint32_t flags) {
   if (n == 0) return STL_OK;
@@ -252,7 +297,9 @@ void stl_shutdown(void) {
     std::lock_guard<std::mutex> dl(d->mu);
     (void)hipSetDevice(d->ordinal);
     (void)hipStreamSynchronize(d->stream);
-    for (DevBuf* b : {&d->ws, &d->sig, &d->msg, &d->pk, &d->bitmap, &d->pre, &d->off, &d->len, &d->ctr}) b->release();
+    for (DevBuf* b : {&d->ws, &d->sig, &d->msg, &d->pk, &d->bitmap, &d->pre, &d->off, &d->len, &d->ctr, &d->txid,
+                      &d->status})
+      b->release();
     for (auto& kv : d->stream_ws) kv.second->release();
     for (auto& kv : d->stream_ctr) kv.second->release();
     (void)hipStreamDestroy(d->stream);
@@ -288,6 +335,37 @@ int stl_ed25519_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8
 int stl_tx_verify_batch(const uint8_t* preimages, const uint64_t* offset, const uint32_t* len, const uint8_t* sig,
                         const uint8_t* pk, size_t n, uint8_t* accept_bitmap, uint32_t flags) {
   return run_batch(sig, nullptr, pk, preimages, offset, len, n, accept_bitmap, flags);
+}
+
+int stl_tx_blob_verify_batch(const uint8_t* blobs, const uint64_t* offset, const uint32_t* len, size_t n,
+                             uint8_t* accept_bitmap, uint8_t* status, uint8_t* tx_id, uint32_t flags) {
+  if (n == 0) return STL_OK;
+  if (!blobs || !offset || !len || !accept_bitmap) return STL_EINVAL;
+  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) return STL_EINVAL;
+  int rc = ensure_init();
+  if (rc) return rc;
+  const uint32_t policy = stl::kernel_mode(flags);
+  const int g = (int)g_devs.size();
+  if (g == 0) return STL_ENODEV;
+  const size_t kMaxShard = (size_t)1 << 31;
+  const int gg = (int)std::max<size_t>((size_t)g, (n + kMaxShard - 1) / kMaxShard);
+  std::vector<int> rcs(gg, STL_OK);
+  std::vector<std::thread> th;
+  for (int r = 0; r < gg; ++r) {
+    size_t lo, hi;
+    shard(n, r, gg, &lo, &hi);
+    if (gg == 1) {
+      rcs[r] = run_blob_shard(*g_devs[0], blobs, offset, len, lo, hi, accept_bitmap, status, tx_id, policy);
+    } else {
+      th.emplace_back([&, r, lo, hi]() {
+        rcs[r] = run_blob_shard(*g_devs[r % g], blobs, offset, len, lo, hi, accept_bitmap, status, tx_id, policy);
+      });
+    }
+  }
+  for (auto& t : th) t.join();
+  for (int r : rcs)
+    if (r) return r;
+  return STL_OK;
 }
 
 int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned long long mlen, const uint8_t* pk) {
@@ -358,6 +436,25 @@ int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offse
   uint32_t* ctr = nullptr;
   if ((rc = stream_counter(d, s, &ctr))) return rc;
   STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(d), s));
+  return STL_OK;
+}
+
+int stl_tx_blob_prepare_device(const uint8_t* d_blobs, const uint64_t* d_offset, const uint32_t* d_len, size_t n,
+                               uint8_t* d_msg, uint8_t* d_sig, uint8_t* d_pk, uint8_t* d_tx_id, uint8_t* d_status,
+                               void* stream) {
+  if (n == 0) return STL_OK;
+  if (!d_blobs || !d_offset || !d_len || !d_msg || !d_sig || !d_pk || !d_status || n > 0xffffffc0ull)
+    return STL_EINVAL;
+  int rc = ensure_init();
+  if (rc) return rc;
+  const int di = current_device_index();
+  if (di < 0) return STL_ENODEV;
+  Device& d = *g_devs[di];
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* ctr = nullptr;
+  if ((rc = stream_counter(d, s, &ctr))) return rc;
+  STL_TRY(stl::launch_tx_blob(d_blobs, d_offset, d_len, (uint32_t)n, d_msg, d_sig, d_pk, d_tx_id, d_status, ctr,
+                              hash_grid(d), s));
   return STL_OK;
 }
 

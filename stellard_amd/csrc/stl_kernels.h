@@ -34,6 +34,9 @@ hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t*
 // bound on workgroups (the kernel pulls work from the counter)
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint32_t* counter, uint32_t grid, hipStream_t stream);
+hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
+                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* counter, uint32_t grid,
+                          hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
                        uint32_t grid, hipStream_t stream);
 

@@ -10,6 +10,9 @@
 //   hram_var_kernel       k for arbitrary-length messages.
 //   tx_hash_kernel        SHA512Half(signing preimage) per transaction
 //                         (Serializer.cpp:354-360 / SerializedObject.cpp:444-450).
+//   tx_blob_kernel        from serialized transactions: canonical-form pass,
+//                         signing hash by splice, transaction ID, verify inputs
+//                         (stl_txblob.h).
 //   sign_kernel           RFC 8032 keypair + signature (synthetic data only).
 //
 // Launch geometry: 256-thread workgroups (4 waves); phases 2 and 3 use a grid
@@ -18,6 +21,7 @@
 // resident lanes.
 #include "stl_base_table.h"
 #include "stl_kernels.h"
+#include "stl_txblob.h"
 #include "stl_verify_core.h"
 
 // Occupancy target of the verify kernel (waves per SIMD); register budget =
@@ -246,6 +250,111 @@ __global__ __launch_bounds__(kBlock) void tx_hash_kernel(const uint8_t* __restri
   }
 }
 
+// Serialized transactions -> verify inputs.  Same work queue as
+// tx_hash_kernel; a lane runs the canonical-form pass when it takes a blob,
+// then one SHA-512 block per iteration: first the signing hash
+// ("STX\0" || blob minus the cut fields), then, if requested, the transaction
+// ID ("TXN\0" || blob).  A lane whose blob is deferred or malformed writes a
+// signature the verify kernels always reject (S = 2^256 - 1) and a zero key.
+__global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restrict__ blobs,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ len, uint32_t n,
+                                                         uint8_t* __restrict__ msg, uint8_t* __restrict__ sig,
+                                                         uint8_t* __restrict__ pk, uint8_t* __restrict__ txid,
+                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ counter) {
+  const uint32_t lane = threadIdx.x & 63u;
+  SpliceStream ss;
+  ss.init(blobs, 0, kPrefixTxSign, nullptr);
+  uint64_t st[8];
+  sha512_init(st);
+  uint32_t mi = 0, blk = 0, nb = 0, phase = 0;
+  bool active = false, exhausted = false;
+  for (;;) {
+    const uint64_t need = __ballot(!active);
+    if (need != 0 && !exhausted) {  // wave-uniform
+      const int leader = __ffsll((unsigned long long)need) - 1;
+      uint32_t base = 0;
+      if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(need));
+      base = __shfl(base, leader);
+      exhausted = base + (uint32_t)__popcll(need) >= n;
+      if (!active) {
+        mi = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+        if (mi < n) {
+          const uint8_t* b = blobs + off[mi];
+          const uint32_t L = len[mi];
+          TxLayout t;
+          tx_blob_parse(b, L, t);
+          status[mi] = (uint8_t)t.status;
+          uint4* sq = reinterpret_cast<uint4*>(sig + 64 * (size_t)mi);
+          if (t.status == kTxOk) {
+            uint32_t sgw[16], pkw[8];
+            blob_words(sgw, b, t.sig_off, 16, L);
+            blob_words(pkw, b, t.pk_off, 8, L);
+            sq[0] = make_uint4(sgw[0], sgw[1], sgw[2], sgw[3]);
+            sq[1] = make_uint4(sgw[4], sgw[5], sgw[6], sgw[7]);
+            sq[2] = make_uint4(sgw[8], sgw[9], sgw[10], sgw[11]);
+            sq[3] = make_uint4(sgw[12], sgw[13], sgw[14], sgw[15]);
+            st8(pk + 32 * (size_t)mi, pkw);
+            ss.init(b, L, kPrefixTxSign, &t);
+            phase = 0;
+          } else {
+            const uint4 z = make_uint4(0u, 0u, 0u, 0u), f = make_uint4(~0u, ~0u, ~0u, ~0u);
+            sq[0] = z; sq[1] = z; sq[2] = f; sq[3] = f;
+            uint4* pq = reinterpret_cast<uint4*>(pk + 32 * (size_t)mi);
+            pq[0] = z; pq[1] = z;
+            uint4* mq = reinterpret_cast<uint4*>(msg + 32 * (size_t)mi);
+            mq[0] = z; mq[1] = z;
+            ss.init(b, L, kPrefixTxId, nullptr);
+            phase = 1;
+          }
+          if (t.status == kTxDeferred || (phase == 1 && txid == nullptr)) {
+            if (txid != nullptr) {
+              uint4* tq = reinterpret_cast<uint4*>(txid + 32 * (size_t)mi);
+              tq[0] = make_uint4(0u, 0u, 0u, 0u);
+              tq[1] = make_uint4(0u, 0u, 0u, 0u);
+            }
+          } else {
+            nb = ss.blocks();
+            blk = 0;
+            sha512_init(st);
+            active = true;
+          }
+        }
+      }
+    }
+    if (!__any(active)) break;
+    if (active) {
+      uint64_t w[16];
+      ss.block(w, blk, blk + 1 == nb);
+      sha512_compress(st, w);
+      if (++blk == nb) {
+        uint32_t h[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          h[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+          h[2 * j + 1] = bswap32((uint32_t)st[j]);
+        }
+        if (phase == 0) {
+          st8(msg + 32 * (size_t)mi, h);
+          if (txid != nullptr) {
+            const uint8_t* b = blobs + off[mi];
+            ss.init(b, len[mi], kPrefixTxId, nullptr);
+            nb = ss.blocks();
+            blk = 0;
+            sha512_init(st);
+            phase = 1;
+          } else {
+            active = false;
+          }
+        } else {
+          st8(txid + 32 * (size_t)mi, h);
+          active = false;
+        }
+      }
+    }
+  }
+}
+
 // SHA-512 of a short word-aligned input (nwords even, nwords*4 <= 108 bytes).
 __device__ __forceinline__ void sha512_short(uint32_t out[16], const uint32_t* in, int nwords) {
   uint64_t st[8], w[16];
@@ -362,6 +471,18 @@ hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_
   const uint32_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(tx_hash_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, pre, off, len, n,
                      msg, counter);
+  return hipGetLastError();
+}
+
+hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
+                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* counter, uint32_t grid,
+                          hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(tx_blob_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, blobs, off, len,
+                     n, msg, sig, pk, txid, status, counter);
   return hipGetLastError();
 }
 

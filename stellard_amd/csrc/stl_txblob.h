@@ -1,0 +1,381 @@
+// stl_txblob.h -- signing hash and transaction ID straight from a serialized
+// transaction (the wire / rawTransaction blob), for the gfx950 kernels and
+// their host build.
+//
+// Reference path:
+//   SerializedTransaction(SerializerIterator&)   SerializedTransaction.cpp:65-92
+//     -> STObject::set                            SerializedObject.cpp:266-306
+//   getSigningHash = SHA512Half("STX\0" || STObject::add(s, false))
+//                                                 SerializedObject.cpp:444-450, 353-379
+//   getTransactionID = SHA512Half("TXN\0" || STObject::add(s, true))
+//                                                 SerializedTransaction.cpp:167-171
+//   checkSign: getFieldVL(sfSigningPubKey), getFieldVL(sfTxnSignature)
+//                                                 SerializedTransaction.cpp:192-230
+//
+// The reference parses the blob into fields and serialises them again, sorted
+// by fieldCode, leaving out the non-signing fields (TxnSignature, Signature,
+// TxnSignatures: FieldNames.cpp:49-51).  When the blob is already in the form
+// that re-serialisation produces ("canonical"), that is the blob itself with
+// those top-level fields cut out, so the kernels splice instead of
+// re-serialising: one pass over the fields checks canonical form and records
+// the cut ranges, and the SHA-512 message stream skips them.  Anything the pass
+// cannot prove canonical is DEFERRED to the caller's own checkSign (a deferral
+// is never a reject).  What the pass checks, per reference rule:
+//   * field headers in the only form addFieldID writes (Serializer.cpp:193-262);
+//   * strictly ascending fieldCode in every object (add() sorts through a
+//     std::map; setType rejects duplicates, SerializedObject.cpp:152-207);
+//   * every field a declared one (SerializeDeclarations.h; undeclared codes the
+//     reference would create on the fly are deferred, not judged);
+//   * nested objects end with 0xE1, arrays with 0xF1, no 0xE1 at top level
+//     (set() stops there and ignores the rest), at most kBlobMaxDepth levels;
+//   * VL lengths in range (decodeVLLength, Serializer.cpp:549-575), Vector256 a
+//     multiple of 32 bytes (STVector256::construct drops a partial tail),
+//     path elements with only the valid type bits, no empty path, and no
+//     account/issuer bit over a zero id (STPathElement recomputes the type
+//     from the ids, SerializedTypes.h:1179-1187);
+//   * length within [txMinSizeBytes, txMaxSizeBytes] (Protocol.h:41-45).
+// Amounts, integers, hashes and VL payloads re-serialise byte for byte from any
+// encoding the reference constructs (STAmount.cpp:465-560), so they need no
+// check beyond their size.
+#pragma once
+#include "stl_sha512.h"
+
+namespace stl {
+
+constexpr uint32_t kPrefixTxSign = 0x53545800u;  // HashPrefix::txSign "STX\0", HashPrefix.cpp:30
+constexpr uint32_t kPrefixTxId = 0x54584E00u;    // HashPrefix::transactionID "TXN\0", HashPrefix.cpp:25
+constexpr uint32_t kTxMinBytes = 32;             // Protocol::txMinSizeBytes
+constexpr uint32_t kTxMaxBytes = 1024 * 1024;    // Protocol::txMaxSizeBytes
+constexpr int kBlobMaxDepth = 8;
+
+// per-transaction status (include/stl.h STL_TX_*)
+constexpr uint32_t kTxOk = 0;         // signing hash computed, verify decides
+constexpr uint32_t kTxDeferred = 1;   // not provably canonical: caller's serial checkSign
+constexpr uint32_t kTxMalformed = 2;  // canonical, but SigningPubKey != 32 B or TxnSignature != 64 B
+                                      // (RippleAddress.cpp:192-194 throws -> checkSign false)
+
+// field codes, FIELD_CODE(type, index) = type << 16 | index
+constexpr uint32_t kCodeSigningPubKey = 0x70003u;  // VL 3
+constexpr uint32_t kCodeTxnSignature = 0x70004u;   // VL 4
+constexpr uint32_t kCodeSignature = 0x70006u;      // VL 6
+constexpr uint32_t kCodeTxnSignatures = 0xF0003u;  // ARRAY 3
+constexpr uint32_t kCodeObjectEnd = 0xE0001u;      // STI_OBJECT, 1
+constexpr uint32_t kCodeArrayEnd = 0xF0001u;       // STI_ARRAY, 1
+
+STL_HD uint64_t name_range(int a, int b) { return ((2ull << b) - 1ull) & ~((1ull << a) - 1ull); }
+
+// Declared field indices per serialized type (SerializeDeclarations.h FIELD
+// lines; all indices are < 64).
+STL_HD uint64_t declared_names(uint32_t type) {
+  switch (type) {
+    case 1: return name_range(1, 2);                                // UINT16
+    case 2: return name_range(2, 34) & ~(1ull << 15);               // UINT32
+    case 3: return name_range(1, 8);                                // UINT64
+    case 4: return 1ull << 1;                                       // HASH128
+    case 5: return name_range(1, 9) | name_range(16, 19);           // HASH256
+    case 6: return name_range(1, 9) | name_range(16, 18);           // AMOUNT
+    case 7: return name_range(1, 13);                               // VL
+    case 8: return name_range(1, 4) | name_range(7, 10);            // ACCOUNT
+    case 14: return name_range(2, 10);                              // OBJECT
+    case 15: return name_range(2, 9);                               // ARRAY
+    case 16: return name_range(1, 3);                               // UINT8
+    case 17: return name_range(1, 4);                               // HASH160
+    case 18: return 1ull << 1;                                      // PATHSET
+    case 19: return name_range(1, 3);                               // VECTOR256
+    default: return 0;
+  }
+}
+
+STL_HD bool field_declared(uint32_t type, uint32_t name) {
+  return name < 64 && ((declared_names(type) >> name) & 1ull) != 0;
+}
+
+// Fixed payload size of a type, 0 for the variable ones.
+STL_HD uint32_t fixed_size(uint32_t type) {
+  switch (type) {
+    case 16: return 1;
+    case 1: return 2;
+    case 2: return 4;
+    case 3: return 8;
+    case 4: return 16;
+    case 17: return 20;
+    case 5: return 32;
+    default: return 0;
+  }
+}
+
+// Result of the canonical-form pass.  Cut ranges are ascending; unused ones
+// are [len, len).
+struct TxLayout {
+  uint32_t status;
+  uint32_t pk_off, pk_len;    // SigningPubKey payload (pk_len 0xffffffff: absent)
+  uint32_t sig_off, sig_len;  // TxnSignature payload
+  uint32_t xs0, xe0, xs1, xe1, xs2, xe2;
+};
+
+STL_HD bool bytes_nonzero(const uint8_t* b, uint32_t pos, uint32_t n) {
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < n; ++i) acc |= b[pos + i];
+  return acc != 0;
+}
+
+// The canonical-form pass over one blob (one lane).  Byte loads only: fields
+// are short and the pass is a few percent of the hashing that follows.
+STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t) {
+  t.status = kTxDeferred;
+  t.pk_off = t.sig_off = 0;
+  t.pk_len = t.sig_len = 0xffffffffu;
+  t.xs0 = t.xe0 = t.xs1 = t.xe1 = t.xs2 = t.xe2 = len;
+  if (len < kTxMinBytes || len > kTxMaxBytes) return;
+  uint32_t last[kBlobMaxDepth + 1];
+  last[0] = 0;
+  uint32_t arrays = 0;  // bit d: level d is an array
+  int depth = 0;
+  int ncut = 0;
+  bool cut_open = false;  // a cut TxnSignatures array still open
+  uint32_t pos = 0;
+  for (;;) {
+    if (pos == len) {
+      if (depth != 0) return;  // unterminated object / array: re-serialisation adds the marker
+      break;
+    }
+    const uint32_t hpos = pos;
+    uint32_t type = b[pos++];
+    uint32_t name = type & 15u;
+    type >>= 4;
+    if (type == 0) {
+      if (pos >= len) return;
+      type = b[pos++];
+      if (type < 16) return;
+    }
+    if (name == 0) {
+      if (pos >= len) return;
+      name = b[pos++];
+      if (name < 16) return;
+    }
+    const uint32_t code = (type << 16) | name;
+    if ((arrays >> depth) & 1u) {
+      // inside an array: an element header (STArray::construct) or the end
+      if (code == kCodeArrayEnd) {
+        --depth;
+        if (depth == 0 && cut_open) {
+          cut_open = false;
+          if (ncut == 1) t.xe0 = pos;
+          else if (ncut == 2) t.xe1 = pos;
+          else t.xe2 = pos;
+        }
+        continue;
+      }
+      if (!field_declared(type, name) || depth == kBlobMaxDepth) return;
+      ++depth;
+      arrays &= ~(1u << depth);
+      last[depth] = 0;
+      continue;
+    }
+    if (code == kCodeObjectEnd) {
+      if (depth == 0) return;  // set() stops at a top-level end marker
+      --depth;
+      continue;
+    }
+    if (!field_declared(type, name) || code <= last[depth]) return;
+    last[depth] = code;
+    const bool cut =
+        depth == 0 && (code == kCodeTxnSignature || code == kCodeSignature || code == kCodeTxnSignatures);
+    if (cut) {
+      // strictly ascending codes: each of the three at most once
+      if (ncut == 0) t.xs0 = hpos;
+      else if (ncut == 1) t.xs1 = hpos;
+      else t.xs2 = hpos;
+      ++ncut;
+    }
+    uint32_t size = fixed_size(type);
+    if (type == 6) {  // AMOUNT: native 8 bytes, else 8 + currency + issuer
+      if (pos >= len) return;
+      size = (b[pos] & 0x80u) ? 48u : 8u;
+    } else if (type == 7 || type == 8 || type == 19) {  // VL, ACCOUNT, VECTOR256
+      if (pos >= len) return;
+      const uint32_t b1 = b[pos++];
+      if (b1 <= 192) {
+        size = b1;
+      } else if (b1 <= 240) {
+        if (pos + 1 > len) return;
+        size = 193u + (b1 - 193u) * 256u + b[pos];
+        pos += 1;
+      } else if (b1 <= 254) {
+        if (pos + 2 > len) return;
+        size = 12481u + (b1 - 241u) * 65536u + (uint32_t)b[pos] * 256u + b[pos + 1];
+        pos += 2;
+      } else {
+        return;
+      }
+      if (type == 19 && (size & 31u) != 0) return;
+      if (depth == 0 && code == kCodeSigningPubKey) {
+        t.pk_off = pos;
+        t.pk_len = size;
+      } else if (depth == 0 && code == kCodeTxnSignature) {
+        t.sig_off = pos;
+        t.sig_len = size;
+      }
+    } else if (type == 18) {  // PATHSET
+      bool empty = true;
+      for (;;) {
+        if (pos >= len) return;
+        const uint32_t e = b[pos++];
+        if (e == 0x00u || e == 0xFFu) {
+          if (empty) return;
+          if (e == 0x00u) break;
+          empty = true;
+          continue;
+        }
+        if (e & ~0x31u) return;
+        const uint32_t need = 20u * (((e >> 0) & 1u) + ((e >> 4) & 1u) + ((e >> 5) & 1u));
+        if (need > len - pos) return;
+        if ((e & 0x01u) && !bytes_nonzero(b, pos, 20)) return;
+        if ((e & 0x01u)) pos += 20;
+        if ((e & 0x10u)) pos += 20;
+        if ((e & 0x20u) && !bytes_nonzero(b, pos, 20)) return;
+        if ((e & 0x20u)) pos += 20;
+        empty = false;
+      }
+      size = 0;
+    } else if (type == 14 || type == 15) {  // OBJECT, ARRAY
+      if (depth == kBlobMaxDepth) return;
+      ++depth;
+      if (type == 15) arrays |= 1u << depth;
+      else arrays &= ~(1u << depth);
+      last[depth] = 0;
+      if (cut) cut_open = true;  // only TxnSignatures (an array) can be open here
+      continue;
+    }
+    if (size > len - pos) return;
+    pos += size;
+    if (cut) {
+      if (ncut == 1) t.xe0 = pos;
+      else if (ncut == 2) t.xe1 = pos;
+      else t.xe2 = pos;
+    }
+  }
+  t.status = (t.pk_len == 32u && t.sig_len == 64u) ? kTxOk : kTxMalformed;
+}
+
+// Message stream prefix(4 bytes) || blob minus up to three cut ranges, as
+// little-endian 32-bit words for SHA-512.  Whole aligned dwords are loaded
+// wherever they lie inside the blob; a byte funnel (acc) joins the pieces.
+struct SpliceStream {
+  const uint8_t* b;
+  uint32_t len, pos, total;
+  uint32_t xs0, xe0, xs1, xe1, xs2, xe2;
+  uint64_t acc;
+  uint32_t nb;
+  bool done;
+
+  STL_HD void init(const uint8_t* blob, uint32_t n, uint32_t prefix, const TxLayout* t) {
+    b = blob;
+    len = n;
+    pos = 0;
+    if (t) {
+      xs0 = t->xs0; xe0 = t->xe0; xs1 = t->xs1; xe1 = t->xe1; xs2 = t->xs2; xe2 = t->xe2;
+    } else {
+      xs0 = xe0 = xs1 = xe1 = xs2 = xe2 = n;
+    }
+    total = 4u + n - (xe0 - xs0) - (xe1 - xs1) - (xe2 - xs2);
+    acc = bswap32(prefix);  // prefix bytes in memory order
+    nb = 4;
+    done = false;
+  }
+  STL_HD void fetch() {
+    while (pos == xs0 && pos < len) {
+      pos = xe0;
+      xs0 = xs1; xe0 = xe1;
+      xs1 = xs2; xe1 = xe2;
+      xs2 = xe2 = len;
+    }
+    if (pos >= len) {
+      done = true;
+      return;
+    }
+    const uint32_t lim = xs0 < len ? xs0 : len;
+    const uint32_t sh = (uint32_t)((uintptr_t)(b + pos) & 3u);
+    uint32_t k = 4u - sh;
+    if (k > lim - pos) k = lim - pos;
+    uint32_t v;
+    if (pos >= sh && pos - sh + 4u <= len) {
+      v = *reinterpret_cast<const uint32_t*>(b + pos - sh) >> (8u * sh);
+    } else {  // the blob's last partial dword, byte by byte
+      v = 0;
+      for (uint32_t i = 0; i < k; ++i) v |= (uint32_t)b[pos + i] << (8u * i);
+    }
+    if (k < 4) v &= (1u << (8u * k)) - 1u;
+    acc |= (uint64_t)v << (8u * nb);
+    nb += k;
+    pos += k;
+  }
+  STL_HD uint32_t word() {
+    while (nb < 4 && !done) fetch();
+    const uint32_t w = (uint32_t)acc;
+    acc >>= 32;
+    nb = nb >= 4 ? nb - 4 : 0;
+    return w;
+  }
+  STL_HD uint32_t blocks() const { return (total + 17u + 127u) / 128u; }
+  // next 128-byte block (blocks are consumed in order) with FIPS 180-4 padding
+  STL_HD void block(uint64_t w[16], uint32_t blk, bool last) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      uint32_t m[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t v = word();
+        const int64_t keep = (int64_t)total - (int64_t)(128u * blk + 4u * (2 * j + h));
+        if (keep < 4) {
+          v = keep <= 0 ? 0u : (v & ((1u << (8 * keep)) - 1u));
+          if (keep >= 0) v |= 0x80u << (8 * keep);
+        }
+        m[h] = v;
+      }
+      w[j] = be64_from_le32(m[0], m[1]);
+    }
+    if (last) {
+      w[14] = 0;
+      w[15] = (uint64_t)total * 8u;
+    }
+  }
+};
+
+// n little-endian words from blob bytes [off, off + 4n) (off unaligned).
+STL_HD void blob_words(uint32_t* out, const uint8_t* b, uint32_t off, uint32_t n, uint32_t len) {
+  const uint32_t sh = (uint32_t)((uintptr_t)(b + off) & 3u);
+  if (off >= sh && (uint64_t)(off - sh) + 4ull * (n + (sh ? 1u : 0u)) <= (uint64_t)len) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(b + off - sh);
+    if (sh == 0) {
+      for (uint32_t i = 0; i < n; ++i) out[i] = q[i];
+    } else {
+      for (uint32_t i = 0; i < n; ++i) out[i] = align_byte(q[i + 1], q[i], sh);
+    }
+  } else {
+    for (uint32_t i = 0; i < n; ++i)
+      out[i] = (uint32_t)b[off + 4 * i] | ((uint32_t)b[off + 4 * i + 1] << 8) |
+               ((uint32_t)b[off + 4 * i + 2] << 16) | ((uint32_t)b[off + 4 * i + 3] << 24);
+  }
+}
+
+// Host-side / test convenience: the whole per-blob computation in one call.
+STL_HD void splice_sha512_half(uint32_t out[8], const uint8_t* blob, uint32_t len, uint32_t prefix,
+                               const TxLayout* t) {
+  SpliceStream s;
+  s.init(blob, len, prefix, t);
+  uint64_t st[8], w[16];
+  sha512_init(st);
+  const uint32_t nb = s.blocks();
+  for (uint32_t k = 0; k < nb; ++k) {
+    s.block(w, k, k + 1 == nb);
+    sha512_compress(st, w);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+    out[2 * j + 1] = bswap32((uint32_t)st[j]);
+  }
+}
+
+}  // namespace stl

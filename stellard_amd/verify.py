@@ -99,6 +99,35 @@ def tx_verify_batch(preimages, sig, pk, policy=POLICY_SODIUM_1_0_18):
     return unpack_bitmap(bitmap, n)
 
 
+def _pack(chunks):
+    n = len(chunks)
+    lens = np.array([len(p) for p in chunks], dtype=np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(bytes(p) for p in chunks) + b"\0" * 4, dtype=np.uint8).copy()
+    return buf, offs, lens
+
+
+TX_OK, TX_DEFERRED, TX_MALFORMED = N.STL_TX_OK, N.STL_TX_DEFERRED, N.STL_TX_MALFORMED
+
+
+def tx_blob_verify_batch(blobs, policy=POLICY_SODIUM_1_0_18, tx_ids=False):
+    """checkSign straight from serialized transactions (list of bytes, each
+    the whole transaction with its TxnSignature).  Returns (accept bool[n],
+    status uint8[n]) -- status TX_OK / TX_DEFERRED / TX_MALFORMED, see
+    include/stl.h -- plus the transaction IDs (n, 32) when ``tx_ids``."""
+    n = len(blobs)
+    buf, offs, lens = _pack(blobs)
+    bitmap = np.zeros((n + 7) // 8 or 1, dtype=np.uint8)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    ids = np.zeros((max(n, 1), 32), dtype=np.uint8) if tx_ids else None
+    N.check(N.load().stl_tx_blob_verify_batch(_buf(buf), _buf(offs), _buf(lens), n, _buf(bitmap), _buf(status),
+                                              _buf(ids) if tx_ids else None, policy), "stl_tx_blob_verify_batch")
+    bits = unpack_bitmap(bitmap, n)
+    return (bits, status[:n], ids[:n]) if tx_ids else (bits, status[:n])
+
+
 # ---- transaction level: SerializedTransaction::checkSign ----
 
 class SignedTx:
@@ -191,6 +220,31 @@ def verify_batch_device(sig, msg, pk, out_words=None, policy=POLICY_SODIUM_1_0_1
         ctypes.c_void_p(sig.data_ptr()), ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(pk.data_ptr()), n,
         ctypes.c_void_p(out_words.data_ptr()), policy, _stream_ptr(stream)), "stl_ed25519_verify_batch_device")
     return out_words
+
+
+def tx_blob_prepare_device(blobs, offsets, lengths, tx_ids=True, stream=None):
+    """Serialized transactions already in HBM (uint8 / int64 / int32 CUDA
+    tensors) -> dict of msg (n,32), sig (n,64), pk (n,32), status (n,) and
+    tx_id (n,32) tensors, asynchronously on ``stream``; follow with
+    verify_batch_device(sig, msg, pk)."""
+    import torch
+    n = offsets.shape[0]
+    dev = blobs.device
+    out = {"msg": torch.empty((n, 32), dtype=torch.uint8, device=dev),
+           "sig": torch.empty((n, 64), dtype=torch.uint8, device=dev),
+           "pk": torch.empty((n, 32), dtype=torch.uint8, device=dev),
+           "status": torch.empty((n,), dtype=torch.uint8, device=dev),
+           "tx_id": torch.empty((n, 32), dtype=torch.uint8, device=dev) if tx_ids else None}
+    for t in (blobs, offsets, lengths):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("device entry point needs contiguous CUDA tensors")
+    if offsets.dtype != torch.int64 or lengths.dtype != torch.int32:
+        raise ValueError("offsets must be int64 and lengths int32")
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    N.check(N.load().stl_tx_blob_prepare_device(
+        ptr(blobs), ptr(offsets), ptr(lengths), n, ptr(out["msg"]), ptr(out["sig"]), ptr(out["pk"]),
+        ptr(out["tx_id"]), ptr(out["status"]), _stream_ptr(stream)), "stl_tx_blob_prepare_device")
+    return out
 
 
 def sign_batch_device(seed, msg, stream=None):

@@ -20,6 +20,7 @@ static void hostemu_check_sub(const stl::fe& a, const stl::fe& b);
 static void hostemu_check_subk(const stl::fe& a, const stl::fe& b, int k);
 
 #include "../../stellard_amd/csrc/stl_base_table.h"
+#include "../../stellard_amd/csrc/stl_txblob.h"
 #include "../../stellard_amd/csrc/stl_verify_core.h"
 
 static double alpha(const stl::fe& a) {
@@ -109,6 +110,34 @@ void hostemu_sha512_half(const uint8_t* p, uint32_t len, uint8_t out[32]) {
   uint32_t o[8];
   stl::sha512_half_words(o, p, len);
   std::memcpy(out, o, 32);
+}
+
+// The device's serialized-transaction pass (stl_txblob.h) for one blob:
+// status, signing hash (splice), transaction ID, and the layout numbers
+// (pk_off, pk_len, sig_off, sig_len, xs0, xe0, xs1, xe1, xs2, xe2).
+void hostemu_tx_blob(const uint8_t* blob, uint32_t len, uint32_t* status, uint8_t msg[32], uint8_t txid[32],
+                     uint32_t layout[10]) {
+  stl::TxLayout t;
+  stl::tx_blob_parse(blob, len, t);
+  *status = t.status;
+  uint32_t h[8];
+  std::memset(msg, 0, 32);
+  std::memset(txid, 0, 32);
+  if (t.status == stl::kTxOk) {
+    stl::splice_sha512_half(h, blob, len, stl::kPrefixTxSign, &t);
+    std::memcpy(msg, h, 32);
+  }
+  if (t.status != stl::kTxDeferred) {
+    stl::splice_sha512_half(h, blob, len, stl::kPrefixTxId, nullptr);
+    std::memcpy(txid, h, 32);
+  }
+  const uint32_t l[10] = {t.pk_off, t.pk_len, t.sig_off, t.sig_len, t.xs0, t.xe0, t.xs1, t.xe1, t.xs2, t.xe2};
+  std::memcpy(layout, l, sizeof l);
+}
+
+// blob_words as the kernel uses it to gather pk / sig (unaligned source)
+void hostemu_blob_words(const uint8_t* blob, uint32_t off, uint32_t n, uint32_t len, uint32_t* out) {
+  stl::blob_words(out, blob, off, n, len);
 }
 
 // e = d * S mod L with signed d (20-byte magnitude, sign), S 32 bytes.

@@ -17,6 +17,24 @@ def _buf(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+class TxInfo(ctypes.Structure):
+    _fields_ = [("signing_len", ctypes.c_size_t), ("full_len", ctypes.c_size_t),
+                ("pk_len", ctypes.c_long), ("sig_len", ctypes.c_long),
+                ("pk", ctypes.c_uint8 * 64), ("sig", ctypes.c_uint8 * 64),
+                ("max_depth", ctypes.c_int), ("all_declared", ctypes.c_int), ("stopped_early", ctypes.c_int)]
+
+
+def pack_blobs(blobs):
+    """(buffer, offsets u64, lengths u32) for a list of byte strings."""
+    n = len(blobs)
+    lens = np.array([len(b) for b in blobs], np.uint32)
+    offs = np.zeros(n, np.uint64)
+    if n:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(blobs) + b"\0" * 4, np.uint8).copy()
+    return buf, offs, lens
+
+
 class Oracle:
     def __init__(self, lib):
         self.lib = lib
@@ -28,6 +46,9 @@ class Oracle:
         lib.oracle_sha512.argtypes = [V, ctypes.c_size_t, V]
         lib.oracle_seed_keypair.argtypes = [V, V, V]
         lib.oracle_sign.argtypes = [V, V, ctypes.c_size_t, V]
+        lib.oracle_tx_blob.restype = ctypes.c_int
+        lib.oracle_tx_blob.argtypes = [V, ctypes.c_size_t, V, V, ctypes.c_size_t, ctypes.POINTER(TxInfo)]
+        lib.oracle_tx_blob_verify_batch.argtypes = [V, V, V, ctypes.c_size_t, V, V, ctypes.c_uint32, ctypes.c_int]
 
     def verify(self, sig, msg, pk, policy=0):
         return self.lib.oracle_verify(bytes(sig), bytes(msg), len(msg), bytes(pk), policy) == 0
@@ -71,6 +92,25 @@ class Oracle:
         self.lib.oracle_sha512(bytes(data), len(data), out)
         return out.raw
 
+    def tx_blob(self, blob):
+        """Reference re-serialisation of one blob: (ok, info, signing, full)."""
+        cap = len(blob) + 64
+        s = ctypes.create_string_buffer(cap)
+        f = ctypes.create_string_buffer(cap)
+        info = TxInfo()
+        rc = self.lib.oracle_tx_blob(bytes(blob), len(blob), s, f, cap, ctypes.byref(info))
+        return rc == 0, info, s.raw[:info.signing_len], f.raw[:info.full_len]
+
+    def tx_blob_verify_batch(self, blobs, policy=0, threads=0, tx_ids=False):
+        buf, offs, lens = pack_blobs(blobs)
+        n = len(blobs)
+        bm = np.zeros((n + 7) // 8 or 1, np.uint8)
+        ids = np.zeros((max(n, 1), 32), np.uint8)
+        self.lib.oracle_tx_blob_verify_batch(_buf(buf), _buf(offs), _buf(lens), n, _buf(bm),
+                                             _buf(ids) if tx_ids else None, policy, threads)
+        bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+        return (bits, ids[:n]) if tx_ids else bits
+
 
 def _ensure(path, target):
     if not os.path.exists(path):
@@ -102,6 +142,7 @@ def load_sodium_ref():
     lib.ref_crypto_sign_verify_detached.argtypes = [V, V, ctypes.c_ulonglong, V]
     lib.ref_seed_keypair.argtypes = [V, V, V]
     lib.ref_sign_detached.argtypes = [V, V, ctypes.c_ulonglong, V]
+    lib.ref_tx_blob_verify_batch.argtypes = [V, V, V, ctypes.c_size_t, V, V, ctypes.c_uint32, ctypes.c_int]
     if lib.ref_init() != 0:
         return None
     return lib
@@ -115,6 +156,29 @@ def sodium_verify_batch(lib, sig, msg, pk, threads=0):
     bm = np.zeros((n + 7) // 8, np.uint8)
     lib.ref_verify_batch(_buf(sig), _buf(msg), _buf(pk), n, _buf(bm), threads)
     return np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+
+
+def sodium_tx_blob_verify_batch(lib, blobs, threads=0, tx_ids=False):
+    buf, offs, lens = pack_blobs(blobs)
+    n = len(blobs)
+    bm = np.zeros((n + 7) // 8 or 1, np.uint8)
+    ids = np.zeros((max(n, 1), 32), np.uint8)
+    lib.ref_tx_blob_verify_batch(_buf(buf), _buf(offs), _buf(lens), n, _buf(bm), _buf(ids) if tx_ids else None,
+                                 0, threads)
+    bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    return (bits, ids[:n]) if tx_ids else bits
+
+
+def hostemu_tx_blob(lib, blob):
+    """Device pass compiled for the host: (status, msg, txid, layout)."""
+    st = ctypes.c_uint32(0)
+    msg = ctypes.create_string_buffer(32)
+    tid = ctypes.create_string_buffer(32)
+    lay = (ctypes.c_uint32 * 10)()
+    b = bytes(blob) + b"\0" * 4
+    arr = np.frombuffer(b, np.uint8).copy()
+    lib.hostemu_tx_blob(_buf(arr), len(blob), ctypes.byref(st), msg, tid, lay)
+    return st.value, msg.raw, tid.raw, list(lay)
 
 
 def load_hostemu():
@@ -132,4 +196,6 @@ def load_hostemu():
     lib.hostemu_lattice.argtypes = [V, V, V, V]
     lib.hostemu_sc_mul_signed.argtypes = [V, ctypes.c_int, V, V]
     lib.hostemu_sha512_half.argtypes = [V, ctypes.c_uint32, V]
+    lib.hostemu_tx_blob.argtypes = [V, ctypes.c_uint32, V, V, V, V]
+    lib.hostemu_blob_words.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, V]
     return lib

@@ -323,3 +323,101 @@ def test_check_sign_batch_mixed(stl, oracle):
     assert got == exp
     assert all(t.sig_good == e and t.sig_bad == (not e) for t, e in zip(txs, exp))
     assert stl.check_sign_batch(txs) == exp  # cached verdicts
+
+
+# ---- serialized transactions (stl_tx_blob_*; stl_txblob.h) ----
+
+def _blob_expectations(oracle, blobs):
+    """Reference bits / ids (oracle re-serialisation) and the device pass
+    compiled for the host (status) for each blob."""
+    from tests.oracle_bind import hostemu_tx_blob, load_hostemu
+    emu = load_hostemu()
+    bits, ids = oracle.tx_blob_verify_batch(blobs, tx_ids=True)
+    st = np.array([hostemu_tx_blob(emu, b)[0] for b in blobs], np.uint8)
+    return bits, ids, st
+
+
+def _check_blob_results(blobs, got_bits, got_status, got_ids, ref_bits, ref_ids, emu_status):
+    assert np.array_equal(got_status, emu_status), np.nonzero(got_status != emu_status)[0][:10]
+    decided = got_status != 1
+    # decided rows: exactly the reference's checkSign and transaction ID
+    assert np.array_equal(got_bits[decided], ref_bits[decided]), np.nonzero(got_bits != ref_bits)[0][:10]
+    assert (got_ids[decided] == ref_ids[decided]).all()
+    # deferred rows: never accepted, id zero
+    assert not got_bits[~decided].any()
+    assert not got_ids[~decided].any()
+
+
+def test_tx_blob_special_cases_and_corpus(stl, oracle):
+    from tests import txblob as T
+    blobs = [b for _, b, _ in T.special_cases(oracle)] + T.valid_corpus(oracle, 400, seed=21)
+    ref_bits, ref_ids, emu_st = _blob_expectations(oracle, blobs)
+    for policy in (0, 1):
+        bits, st, ids = stl.tx_blob_verify_batch(blobs, policy=policy, tx_ids=True)
+        _check_blob_results(blobs, bits, st, ids, ref_bits, ref_ids, emu_st)
+    assert (emu_st == 0).sum() > 400
+
+
+def test_tx_blob_fuzz(stl, oracle):
+    from tests import txblob as T
+    base = T.valid_corpus(oracle, 200, seed=5)
+    rng = np.random.default_rng(77)
+    blobs = []
+    for _ in range(6000):
+        m = T.mutate(rng, base[int(rng.integers(len(base)))])
+        if rng.random() < 0.3:
+            m = T.mutate(rng, m)
+        blobs.append(m)
+    ref_bits, ref_ids, emu_st = _blob_expectations(oracle, blobs)
+    bits, st, ids = stl.tx_blob_verify_batch(blobs, tx_ids=True)
+    _check_blob_results(blobs, bits, st, ids, ref_bits, ref_ids, emu_st)
+
+
+def test_tx_blob_prepare_device(stl, oracle, torch_cuda):
+    """Device-resident prepare + verify == host entry point; msg / sig / pk as
+    the blob holds them; deferred rows get the always-reject signature."""
+    torch = torch_cuda
+    from tests import txblob as T
+    from tests.oracle_bind import pack_blobs
+    blobs = [b for _, b, _ in T.special_cases(oracle)] + T.valid_corpus(oracle, 300, seed=8, memos=1)
+    buf, offs, lens = pack_blobs(blobs)
+    d_buf = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+    out = stl.tx_blob_prepare_device(d_buf, d_off, d_len)
+    words = stl.verify_batch_device(out["sig"], out["msg"], out["pk"])
+    torch.cuda.synchronize()
+    n = len(blobs)
+    got = stl.words_to_bool(words, n)
+    bits, st, ids = stl.tx_blob_verify_batch(blobs, tx_ids=True)
+    assert np.array_equal(got, bits)
+    assert np.array_equal(out["status"].cpu().numpy(), st)
+    assert np.array_equal(out["tx_id"].cpu().numpy(), ids)
+    sig = out["sig"].cpu().numpy()
+    pk = out["pk"].cpu().numpy()
+    for i, b in enumerate(blobs):
+        if st[i] == 0:
+            ok, info, signing, full = oracle.tx_blob(b)
+            assert bytes(sig[i]) == bytes(info.sig) and bytes(pk[i]) == bytes(info.pk[:32])
+            assert bytes(out["msg"][i].cpu().numpy()) == hashlib.sha512(signing).digest()[:32]
+        else:
+            assert not sig[i, :32].any() and (sig[i, 32:] == 255).all() and not pk[i].any()
+
+
+def test_tx_blob_config5_sizes(stl, oracle):
+    """Ledger-replay shaped blobs (log-uniform 100 B - 4 KB) in one batch of
+    20,000 (SURVEY config 5 ledger size): all accepted, ids and a sample of
+    bits against the oracle."""
+    from tests import txblob as T
+    rng = np.random.default_rng(0x5EED0005)
+    ks = T.keys(oracle, 16, 3)
+    blobs = []
+    for i in range(20000):
+        pk, sk = ks[i % 16]
+        target = int(np.exp(rng.uniform(np.log(100), np.log(4096))))
+        fs = T.payment_fields(rng, pk, i + 1, pad_to=target)
+        blobs.append(T.signed_blob(fs, sk, oracle.sign)[0])
+    bits, st, ids = stl.tx_blob_verify_batch(blobs, tx_ids=True)
+    assert (st == 0).all() and bits.all()
+    for i in rng.choice(len(blobs), 500, replace=False):
+        assert bytes(ids[i]) == T.tx_id(blobs[i])

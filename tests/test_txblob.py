@@ -1,0 +1,147 @@
+"""Serialized-transaction path (stellard_amd/csrc/stl_txblob.h)
+on the CPU: the C re-serialiser (oracle/stl_oracle_tx.c, the reference's
+parse + STObject::add) against an independent Python serializer, and the
+device pass compiled for the host (tests/native/hostemu.cpp) against the
+oracle -- status, signing hash, transaction ID -- on the named special cases
+and on randomly mutated blobs.
+
+Parity anchor: the reference holds no serialized-transaction fixtures (its
+SerializedTransaction_test builds a transaction, signs it and round-trips it:
+SerializedTransaction.cpp:374-400); the two restatements here, plus
+signatures made over the Python preimages and accepted by libsodium, are what
+pin it."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from tests import txblob as T
+from tests.oracle_bind import (hostemu_tx_blob, load_hostemu, load_oracle, load_sodium_ref,
+                               sodium_tx_blob_verify_batch)
+
+OK, DEFERRED, MALFORMED = 0, 1, 2
+MAX_DEPTH = 8
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return load_oracle()
+
+
+@pytest.fixture(scope="module")
+def emu():
+    return load_hostemu()
+
+
+@pytest.fixture(scope="module")
+def corpus(oracle):
+    return T.valid_corpus(oracle, 240, seed=11, with_preimages=True)
+
+
+def h512half(b):
+    return hashlib.sha512(b).digest()[:32]
+
+
+def test_oracle_reserialises_python_blobs(oracle, corpus):
+    blobs, pres = corpus
+    for b, p in zip(blobs, pres):
+        ok, info, signing, full = oracle.tx_blob(b)
+        assert ok
+        assert full == b
+        assert signing == p
+        assert info.pk_len == 32 and info.sig_len == 64
+
+
+def test_corpus_signatures_accepted(oracle, corpus):
+    blobs, _ = corpus
+    bits, ids = oracle.tx_blob_verify_batch(blobs, tx_ids=True)
+    assert bits.all()
+    for b, i in zip(blobs, ids):
+        assert bytes(i) == T.tx_id(b)
+    ref = load_sodium_ref()
+    if ref is not None:
+        rbits, rids = sodium_tx_blob_verify_batch(ref, blobs, tx_ids=True)
+        assert rbits.all()
+        assert (rids == ids).all()
+
+
+def _check_device_vs_oracle(oracle, emu, blob):
+    """Invariants between the device pass and the reference re-serialisation.
+    Returns (device status, oracle-constructible)."""
+    st, msg, tid, lay = hostemu_tx_blob(emu, blob)
+    ok, info, signing, full = oracle.tx_blob(blob)
+    if not ok:
+        return st, False  # the reference never builds this transaction: no claim
+    canonical = full == blob and not info.stopped_early
+    if st != DEFERRED:
+        # the device only decides blobs the reference re-serialises unchanged
+        assert canonical, blob.hex()
+        assert tid == h512half(b"TXN\x00" + full)
+        shaped = info.pk_len == 32 and info.sig_len == 64
+        assert st == (OK if shaped else MALFORMED)
+        if st == OK:
+            assert msg == h512half(signing)
+    elif canonical and info.all_declared and info.max_depth <= MAX_DEPTH:
+        pytest.fail("deferred a canonical blob: " + blob.hex())
+    return st, True
+
+
+def test_device_pass_on_corpus(oracle, emu, corpus):
+    blobs, pres = corpus
+    for b, p in zip(blobs, pres):
+        st, msg, tid, lay = hostemu_tx_blob(emu, b)
+        assert st == OK
+        assert msg == h512half(p)
+        assert tid == T.tx_id(b)
+        pk_off, pk_len, sig_off, sig_len = lay[:4]
+        assert pk_len == 32 and sig_len == 64
+        assert b[pk_off - 2:pk_off] == b"\x73\x20" and b[sig_off - 2:sig_off] == b"\x74\x40"
+
+
+@pytest.mark.parametrize("case", range(len(T.special_cases(load_oracle()))))
+def test_special_cases(oracle, emu, case):
+    name, blob, expect = T.special_cases(oracle)[case]
+    st, constructible = _check_device_vs_oracle(oracle, emu, blob)
+    if expect == "unconstructible":
+        assert not constructible, name
+        return
+    assert constructible, name
+    want = {"ok": OK, "reject": OK, "malformed": MALFORMED, "defer": DEFERRED}[expect]
+    assert st == want, name
+    bit = oracle.tx_blob_verify_batch([blob])[0]
+    if expect != "defer":  # a deferred blob gets the caller's own checkSign, whatever it says
+        assert bit == (expect == "ok"), name
+    if expect == "defer" and name not in ("depth_too_deep", "dynamic_field"):
+        ok, info, signing, full = oracle.tx_blob(blob)
+        assert full != blob or info.stopped_early, name  # deferral was necessary
+
+
+def test_fuzz_invariants(oracle, emu, corpus):
+    blobs, _ = corpus
+    rng = np.random.default_rng(2024)
+    counts = {OK: 0, DEFERRED: 0, MALFORMED: 0}
+    built = 0
+    for _ in range(4000):
+        b = blobs[int(rng.integers(len(blobs)))]
+        m = T.mutate(rng, b)
+        if int(rng.integers(0, 4)) == 0:
+            m = T.mutate(rng, m)
+        st, constructible = _check_device_vs_oracle(oracle, emu, m)
+        counts[st] += 1
+        built += constructible
+    # the mutations reach every outcome
+    assert counts[OK] > 100 and counts[DEFERRED] > 100 and counts[MALFORMED] > 5, counts
+    assert built > 500
+
+
+@pytest.mark.parametrize("off", range(0, 9))
+def test_blob_words_unaligned(emu, off):
+    import ctypes
+    rng = np.random.default_rng(off)
+    buf = np.frombuffer(rng.bytes(128), np.uint8).copy()
+    for n, ln in ((16, 128), (8, off + 32), (8, 128)):
+        if off + 4 * n > ln:
+            continue
+        out = (ctypes.c_uint32 * n)()
+        emu.hostemu_blob_words(buf.ctypes.data_as(ctypes.c_void_p), off, n, ln, out)
+        assert bytes(np.array(out, np.uint32).tobytes()) == buf[off:off + 4 * n].tobytes()
