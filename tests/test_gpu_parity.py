@@ -328,21 +328,28 @@ def test_check_sign_batch_mixed(stl, oracle):
 # ---- serialized transactions (stl_tx_blob_*; stl_txblob.h) ----
 
 def _blob_expectations(oracle, blobs):
-    """Reference bits / ids (oracle re-serialisation) and the device pass
-    compiled for the host (status) for each blob."""
+    """Reference bits / ids (oracle re-serialisation), whether the reference
+    constructs the transaction at all, and the device pass compiled for the
+    host (status, tx id) for each blob."""
     from tests.oracle_bind import hostemu_tx_blob, load_hostemu
     emu = load_hostemu()
     bits, ids = oracle.tx_blob_verify_batch(blobs, tx_ids=True)
-    st = np.array([hostemu_tx_blob(emu, b)[0] for b in blobs], np.uint8)
-    return bits, ids, st
+    built = np.array([oracle.tx_blob(b)[0] for b in blobs], bool)
+    em = [hostemu_tx_blob(emu, b) for b in blobs]
+    st = np.array([e[0] for e in em], np.uint8)
+    emu_ids = np.array([np.frombuffer(e[2], np.uint8) for e in em]).reshape(-1, 32)
+    return dict(bits=bits, ids=ids, built=built, status=st, emu_ids=emu_ids)
 
 
-def _check_blob_results(blobs, got_bits, got_status, got_ids, ref_bits, ref_ids, emu_status):
-    assert np.array_equal(got_status, emu_status), np.nonzero(got_status != emu_status)[0][:10]
+def _check_blob_results(got_bits, got_status, got_ids, exp):
+    # the GPU runs the same pass as its host build, bit for bit
+    assert np.array_equal(got_status, exp["status"]), np.nonzero(got_status != exp["status"])[0][:10]
+    assert np.array_equal(got_ids, exp["emu_ids"])
     decided = got_status != 1
-    # decided rows: exactly the reference's checkSign and transaction ID
-    assert np.array_equal(got_bits[decided], ref_bits[decided]), np.nonzero(got_bits != ref_bits)[0][:10]
-    assert (got_ids[decided] == ref_ids[decided]).all()
+    # decided rows the reference constructs: exactly its checkSign and transaction ID
+    chk = decided & exp["built"]
+    assert np.array_equal(got_bits[chk], exp["bits"][chk]), np.nonzero((got_bits != exp["bits"]) & chk)[0][:10]
+    assert (got_ids[chk] == exp["ids"][chk]).all()
     # deferred rows: never accepted, id zero
     assert not got_bits[~decided].any()
     assert not got_ids[~decided].any()
@@ -351,11 +358,11 @@ def _check_blob_results(blobs, got_bits, got_status, got_ids, ref_bits, ref_ids,
 def test_tx_blob_special_cases_and_corpus(stl, oracle):
     from tests import txblob as T
     blobs = [b for _, b, _ in T.special_cases(oracle)] + T.valid_corpus(oracle, 400, seed=21)
-    ref_bits, ref_ids, emu_st = _blob_expectations(oracle, blobs)
+    exp = _blob_expectations(oracle, blobs)
     for policy in (0, 1):
         bits, st, ids = stl.tx_blob_verify_batch(blobs, policy=policy, tx_ids=True)
-        _check_blob_results(blobs, bits, st, ids, ref_bits, ref_ids, emu_st)
-    assert (emu_st == 0).sum() > 400
+        _check_blob_results(bits, st, ids, exp)
+    assert (exp["status"] == 0).sum() > 400
 
 
 def test_tx_blob_fuzz(stl, oracle):
@@ -368,9 +375,10 @@ def test_tx_blob_fuzz(stl, oracle):
         if rng.random() < 0.3:
             m = T.mutate(rng, m)
         blobs.append(m)
-    ref_bits, ref_ids, emu_st = _blob_expectations(oracle, blobs)
+    exp = _blob_expectations(oracle, blobs)
     bits, st, ids = stl.tx_blob_verify_batch(blobs, tx_ids=True)
-    _check_blob_results(blobs, bits, st, ids, ref_bits, ref_ids, emu_st)
+    _check_blob_results(bits, st, ids, exp)
+    assert exp["built"].sum() > 1000
 
 
 def test_tx_blob_prepare_device(stl, oracle, torch_cuda):

@@ -326,6 +326,8 @@ def special_cases(oracle, seed=7):
 def mutate(rng, blob):
     """One random structural mutation (fuzzing)."""
     b = bytearray(blob)
+    if not b:
+        return bytes(rng.bytes(int(rng.integers(0, 40))))
     k = int(rng.integers(0, 6))
     i = int(rng.integers(0, len(b)))
     if k == 0:
