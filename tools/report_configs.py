@@ -55,6 +55,13 @@ class CpuRef:
     def verify(self, sig, msg, pk, threads):
         return self.ob.sodium_verify_batch(self.lib, sig, msg, pk, threads=threads)
 
+    def tx_blob_verify(self, buf, offs, lens, threads):
+        n = lens.shape[0]
+        bm = np.zeros((n + 7) // 8, np.uint8)
+        B = lambda a: np.ascontiguousarray(a).ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        self.lib.ref_tx_blob_verify_batch(B(buf), B(offs), B(lens), n, B(bm), None, 0, threads)
+        return np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+
     def tx_verify(self, blob, offs, lens, sig, pk, threads):
         n = sig.shape[0]
         bm = np.zeros((n + 7) // 8, np.uint8)
@@ -230,7 +237,10 @@ def tx_config(gpu, cpu, n, rng, pad_lens, cpu_samples):
     def run(lo, hi, threads):
         return cpu.tx_verify(blob, offs[lo:hi], lens[lo:hi], sig_np[lo:hi], pk_np[lo:hi], threads)
 
+    log("  from serialized transactions")
+    from_blobs = blob_leg(gpu, cpu, blobs_from_preimages(pre, sig_np, pk_np), cpu_samples)
     return {
+        "from_serialized_transactions": from_blobs,
         "n": n, "preimage_bytes": {"min": int(lens.min()), "median": int(np.median(lens)), "max": int(lens.max()),
                                    "total": int(lens.sum())},
         "gpu_device_resident_tx_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
@@ -241,6 +251,67 @@ def tx_config(gpu, cpu, n, rng, pad_lens, cpu_samples):
                           "accepted": int(ref_bits.sum())},
         "cpu_full_run_16_threads_s": ref_s,
     }
+
+
+def blobs_from_preimages(pre, sig_np, pk_np):
+    """Whole serialized transactions: the preimage without "STX\\0" with the
+    TxnSignature field (0x74 0x40 <64 B>) put after SigningPubKey, as
+    STObject::add(s, true) orders them."""
+    out = []
+    for i, p in enumerate(pre):
+        k = p.index(b"\x73\x20" + pk_np[i].tobytes()) + 34
+        out.append(p[4:k] + b"\x74\x40" + sig_np[i].tobytes() + p[k:])
+    return out
+
+
+def blob_leg(gpu, cpu, blobs, cpu_samples):
+    """checkSign from serialized transactions: libstl's canonical-form pass +
+    spliced signing hash + transaction ID + verify, vs the reference path
+    (parse, re-serialise, OpenSSL SHA512, libsodium) on the CPU."""
+    t = gpu.torch
+    buf, offs, lens = pack(blobs)
+    buf = np.concatenate([buf, np.zeros(4, np.uint8)])
+    n = len(blobs)
+    d_buf = t.from_numpy(buf).cuda()
+    d_off = t.from_numpy(offs.view(np.int64)).cuda()
+    d_len = t.from_numpy(lens.view(np.int32)).cuda()
+    words = t.empty((n + 63) // 64, dtype=t.int64, device="cuda")
+    times = []
+    for _ in range(6):
+        a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+        a.record(gpu.stream)
+        o = gpu.V.tx_blob_prepare_device(d_buf, d_off, d_len, tx_ids=True, stream=gpu.stream)
+        gpu.V.verify_batch_device(o["sig"], o["msg"], o["pk"], out_words=words, stream=gpu.stream)
+        b.record(gpu.stream)
+        t.cuda.synchronize()
+        times.append(a.elapsed_time(b) * 1e-3)
+    dev_bits = gpu.V.words_to_bool(words, n)
+    status = o["status"].cpu().numpy()
+    dev_s = float(np.median(times[1:]))
+    # prepare kernel alone (canonical pass + both hashes)
+    ptimes = []
+    for _ in range(4):
+        a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+        a.record(gpu.stream)
+        gpu.V.tx_blob_prepare_device(d_buf, d_off, d_len, tx_ids=True, stream=gpu.stream)
+        b.record(gpu.stream)
+        t.cuda.synchronize()
+        ptimes.append(a.elapsed_time(b) * 1e-3)
+    gpu.V.tx_blob_verify_batch(blobs[:1024])
+    (hbits, hst), host_s = timed(lambda: gpu.V.tx_blob_verify_batch(blobs))
+    ref_bits, ref_s = timed(lambda: cpu.tx_blob_verify(buf, offs, lens, 16))
+
+    def run(lo, hi, threads):
+        return cpu.tx_blob_verify(buf, offs[lo:hi], lens[lo:hi], threads)
+
+    return {"n": n, "blob_bytes": {"min": int(lens.min()), "median": int(np.median(lens)), "max": int(lens.max())},
+            "gpu_device_resident_tx_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
+            "gpu_prepare_kernel_ms": float(np.median(ptimes[1:])) * 1e3,
+            "gpu_host_api_tx_per_s": n / host_s,
+            "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
+            "cpu_reference": cpu_rates(run, n, cpu_samples),
+            "bitmap_parity": {"rows": n, "mismatches_device": int((dev_bits != ref_bits).sum()),
+                              "mismatches_host_api": int((hbits != ref_bits).sum()), "accepted": int(ref_bits.sum())}}
 
 
 def config2(gpu, cpu):
