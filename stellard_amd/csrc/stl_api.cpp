@@ -102,14 +102,15 @@ int stream_workspace(Device& d, hipStream_t s, uint4** ws) {
   return STL_OK;
 }
 
-// One-word work counter for (device, stream) of the device-resident tx hash.
-int stream_counter(Device& d, hipStream_t s, uint32_t** ctr) {
+// Work-queue workspace for (device, stream) of the device-resident hash
+// kernels (counter + longest-first order, stl::hash_queue_bytes(n)).
+int stream_queue(Device& d, hipStream_t s, size_t n, uint32_t** qws) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
   auto& slot = d.stream_ctr[s];
   if (!slot) slot.reset(new DevBuf());
-  int rc = slot->ensure(256);
+  int rc = slot->ensure(stl::hash_queue_bytes(n));
   if (rc) return rc;
-  *ctr = static_cast<uint32_t*>(slot->p);
+  *qws = static_cast<uint32_t*>(slot->p);
   return STL_OK;
 }
 
@@ -159,7 +160,7 @@ int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t
     }
     const size_t bytes = (size_t)(end - base);
     if ((rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
-        (rc = d.ctr.ensure(256)))
+        (rc = d.ctr.ensure(stl::hash_queue_bytes(n))))
       return rc;
     if (bytes) STL_TRY(hipMemcpyAsync(d.pre.p, pre + base, bytes, hipMemcpyHostToDevice, s));
     STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, s));
@@ -201,7 +202,7 @@ int run_blob_shard(Device& d, const uint8_t* blobs, const uint64_t* off, const u
   if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(n * 64)) ||
       (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)) ||
       (rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
-      (rc = d.ctr.ensure(256)) || (rc = d.status.ensure(n)) || (txid && (rc = d.txid.ensure(n * 32))))
+      (rc = d.ctr.ensure(stl::hash_queue_bytes(n))) || (rc = d.status.ensure(n)) || (txid && (rc = d.txid.ensure(n * 32))))
     return rc;
   hipStream_t s = d.stream;
   if (bytes) STL_TRY(hipMemcpyAsync(d.pre.p, blobs + base, bytes, hipMemcpyHostToDevice, s));
@@ -434,7 +435,7 @@ int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offse
   Device& d = *g_devs[di];
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t* ctr = nullptr;
-  if ((rc = stream_counter(d, s, &ctr))) return rc;
+  if ((rc = stream_queue(d, s, n, &ctr))) return rc;
   STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(d), s));
   return STL_OK;
 }
@@ -452,7 +453,7 @@ int stl_tx_blob_prepare_device(const uint8_t* d_blobs, const uint64_t* d_offset,
   Device& d = *g_devs[di];
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t* ctr = nullptr;
-  if ((rc = stream_counter(d, s, &ctr))) return rc;
+  if ((rc = stream_queue(d, s, n, &ctr))) return rc;
   STL_TRY(stl::launch_tx_blob(d_blobs, d_offset, d_len, (uint32_t)n, d_msg, d_sig, d_pk, d_tx_id, d_status, ctr,
                               hash_grid(d), s));
   return STL_OK;

@@ -32,10 +32,14 @@ hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t*
                            const uint64_t* mlen, uint32_t n, uint8_t* k_out, hipStream_t stream);
 // counter: one device word of scratch (reset by the launcher); grid: upper
 // bound on workgroups (the kernel pulls work from the counter)
+// Hash-kernel queue workspace: a header (work counter, bucket counts and
+// cursors of the longest-first order) and the order itself.
+constexpr size_t kQueueHeaderBytes = 1024;
+inline size_t hash_queue_bytes(size_t n) { return kQueueHeaderBytes + 4 * n; }
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          uint32_t* counter, uint32_t grid, hipStream_t stream);
+                          uint32_t* qws, uint32_t grid, hipStream_t stream);
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* counter, uint32_t grid,
+                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
                           hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
                        uint32_t grid, hipStream_t stream);

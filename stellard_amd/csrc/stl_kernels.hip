@@ -32,6 +32,11 @@
 #ifndef STL_PRE_WAVES_PER_SIMD
 #define STL_PRE_WAVES_PER_SIMD 2
 #endif
+// Hash kernels: waves per SIMD (SHA-512 rounds are a serial chain per lane,
+// so occupancy hides the VALU and memory latency).
+#ifndef STL_HASH_WAVES_PER_SIMD
+#define STL_HASH_WAVES_PER_SIMD 4
+#endif
 
 namespace stl {
 
@@ -196,16 +201,127 @@ __global__ void hram_var_kernel(const uint8_t* __restrict__ sig, const uint8_t* 
   st8(k_out + 32 * (size_t)i, k);
 }
 
+// ---- wave-cooperative message windows for the hash kernels ----
+// Each lane hashes its own message, so a lane-private dword load touches 64
+// different cache lines per instruction and the blocks are re-read from L2
+// once per dword.  Instead, every iteration the wave fills, for each lane, a
+// 144-byte window at a 16-byte aligned address of that lane's choosing:
+// consecutive lanes load consecutive 16-byte chunks of one lane's window (so
+// one load instruction covers ~9 lines), through LDS, and each lane then reads
+// its 128-byte block from its own window.  Chunks wholly past the message end
+// are not loaded; the 16-byte granules holding the first and last message
+// bytes are read whole.
+constexpr uint32_t kWinChunks = 9;  // 144 bytes: a 128-byte block at any alignment
+constexpr uint32_t kWinBytes = 16 * kWinChunks;
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// win: this wave's 64 * kWinChunks uint4; base == 0 marks an idle lane.
+// Only granules that hold bytes of [lo, end) are loaded.
+__device__ __forceinline__ void wave_window_fill(uint4* win, uintptr_t base, uintptr_t lo, uintptr_t end,
+                                                 uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 0; k < kWinChunks; ++k) {
+    const uint32_t g = k * 64u + lane;
+    const uint32_t src = g / kWinChunks;
+    const uint32_t c = g - src * kWinChunks;
+    const uintptr_t b = (uintptr_t)shfl_u64(base, src), e = (uintptr_t)shfl_u64(end, src);
+    const uintptr_t l = (uintptr_t)shfl_u64(lo, src);
+    const uintptr_t a = b + 16u * c;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (b != 0 && a < e && a + 16u > l) v = *reinterpret_cast<const uint4*>(a);
+    win[g] = v;  // = window of lane src, chunk c
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Dword source over a lane's window, global loads outside it.
+struct WinSrc {
+  const uint32_t* w;  // this lane's kWinBytes / 4 words in LDS
+  uintptr_t base;
+  const uint32_t* q;  // ByteStream: aligned start of the message
+  __device__ uint32_t at(uintptr_t a) const {
+    const uintptr_t off = a - base;
+    return off < kWinBytes ? w[off >> 2] : *reinterpret_cast<const uint32_t*>(a);
+  }
+  __device__ uint32_t operator()(uint32_t idx) const { return at((uintptr_t)(q + idx)); }
+  __device__ uint32_t operator()(const uint8_t* a) const { return at((uintptr_t)a); }
+};
+
+// ---- longest-first order for the hash work queues ----
+// A 1M-transaction batch is only ~4 messages per resident lane, so a lane that
+// draws a 4 KB message (33 blocks) near the end of the queue sets the tail.
+// A counting sort by SHA-512 block count (64 buckets, longest first) makes the
+// queue hand out long messages first; the last draws are all short.
+constexpr uint32_t kOrderBuckets = 64;
+
+__device__ __forceinline__ uint32_t order_bucket(uint32_t bytes) {
+  const uint32_t nb = (bytes + 17u + 127u) >> 7;
+  return (kOrderBuckets - 1u) - (nb < kOrderBuckets - 1u ? nb : kOrderBuckets - 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void order_count_kernel(const uint32_t* __restrict__ len, uint32_t n,
+                                                             uint32_t extra, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kOrderBuckets];
+  if (threadIdx.x < kOrderBuckets) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+    atomicAdd(&h[order_bucket(len[i] + extra)], 1u);
+  __syncthreads();
+  if (threadIdx.x < kOrderBuckets && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// exclusive scan of the 64 bucket counts into bucket cursors (one wave)
+__global__ __launch_bounds__(64) void order_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor) {
+  const uint32_t t = threadIdx.x;
+  uint32_t v = hist[t];
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)v, d);
+    if (t >= (uint32_t)d) v += u;
+  }
+  cursor[t] = v - hist[t];
+}
+
+__global__ __launch_bounds__(kBlock) void order_scatter_kernel(const uint32_t* __restrict__ len, uint32_t n,
+                                                               uint32_t extra, uint32_t* __restrict__ cursor,
+                                                               uint32_t* __restrict__ order) {
+  __shared__ uint32_t h[kOrderBuckets], base[kOrderBuckets];
+  for (uint32_t tile = blockIdx.x * kBlock; tile < n; tile += gridDim.x * kBlock) {
+    if (threadIdx.x < kOrderBuckets) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = tile + threadIdx.x;
+    uint32_t b = 0, pos = 0;
+    if (i < n) {
+      b = order_bucket(len[i] + extra);
+      pos = atomicAdd(&h[b], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kOrderBuckets && h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], h[threadIdx.x]);
+    __syncthreads();
+    if (i < n) order[base[b] + pos] = i;
+    __syncthreads();
+  }
+}
+
 // msg_i = SHA512Half(preimage_i) (Serializer.cpp:354-360 via
 // STObject::getSigningHash, SerializedObject.cpp:444-450).  Lanes pull
 // preimages from a global counter and advance one 128-byte block per
 // iteration, refilling as they finish: waves stay full whatever the length
 // mix (config 5: 100 B - 4 KB, log-uniform), with no sort pass.
-__global__ __launch_bounds__(kBlock) void tx_hash_kernel(const uint8_t* __restrict__ pre,
+__global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_hash_kernel(const uint8_t* __restrict__ pre,
                                                          const uint64_t* __restrict__ off,
                                                          const uint32_t* __restrict__ len, uint32_t n,
-                                                         uint8_t* __restrict__ msg, uint32_t* __restrict__ counter) {
+                                                         uint8_t* __restrict__ msg, uint32_t* __restrict__ counter,
+                                                         const uint32_t* __restrict__ order) {
+  __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
+  uint4* win = win_all[threadIdx.x >> 6];
   ByteStream bs;
   bs.init(pre, 0);
   uint64_t st[8];
@@ -223,6 +339,7 @@ __global__ __launch_bounds__(kBlock) void tx_hash_kernel(const uint8_t* __restri
       if (!active) {
         mi = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
         if (mi < n) {
+          mi = order[mi];
           bs.init(pre + off[mi], len[mi]);
           nb = bs.blocks();
           blk = 0;
@@ -232,9 +349,14 @@ __global__ __launch_bounds__(kBlock) void tx_hash_kernel(const uint8_t* __restri
       }
     }
     if (!__any(active)) break;
+    const uintptr_t blk_addr = (uintptr_t)(bs.q + 32 * blk);
+    const uintptr_t wbase = active ? (blk_addr & ~(uintptr_t)15) : 0;
+    wave_window_fill(win, wbase, (uintptr_t)bs.p, (uintptr_t)(bs.p + bs.len), lane);
     if (active) {
       uint64_t w[16];
-      bs.block(w, blk, blk + 1 == nb);
+      block_from_window(w, reinterpret_cast<const uint32_t*>(win) + lane * (kWinBytes / 4),
+                        (uint32_t)(blk_addr & 15u) >> 2, bs.mis, (int32_t)bs.len - (int32_t)(128 * blk),
+                        blk + 1 == nb, bs.len, false, false, 0u);
       sha512_compress(st, w);
       if (++blk == nb) {
         uint32_t h[8];
@@ -256,18 +378,26 @@ __global__ __launch_bounds__(kBlock) void tx_hash_kernel(const uint8_t* __restri
 // ("STX\0" || blob minus the cut fields), then, if requested, the transaction
 // ID ("TXN\0" || blob).  A lane whose blob is deferred or malformed writes a
 // signature the verify kernels always reject (S = 2^256 - 1) and a zero key.
-__global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restrict__ blobs,
+__global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kernel(const uint8_t* __restrict__ blobs,
                                                          const uint64_t* __restrict__ off,
                                                          const uint32_t* __restrict__ len, uint32_t n,
                                                          uint8_t* __restrict__ msg, uint8_t* __restrict__ sig,
                                                          uint8_t* __restrict__ pk, uint8_t* __restrict__ txid,
-                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ counter) {
+                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ counter,
+                                                         const uint32_t* __restrict__ order) {
+  __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
-  SpliceStream ss;
+  uint4* win = win_all[threadIdx.x >> 6];
+  SpliceStream ss;  // phase 0: "STX\0" || blob minus the cut fields
+  ByteStream bs;    // phase 1: the 4 bytes before the blob || blob, word 0 -> "TXN\0"
   ss.init(blobs, 0, kPrefixTxSign, nullptr);
+  bs.init(blobs, 0);
+  const uint32_t txn_le = bswap32(kPrefixTxId);
   uint64_t st[8];
   sha512_init(st);
   uint32_t mi = 0, blk = 0, nb = 0, phase = 0;
+  const uint8_t* b = blobs;
+  const uint8_t* bend = blobs;
   bool active = false, exhausted = false;
   for (;;) {
     const uint64_t need = __ballot(!active);
@@ -280,8 +410,10 @@ __global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restri
       if (!active) {
         mi = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
         if (mi < n) {
-          const uint8_t* b = blobs + off[mi];
+          mi = order[mi];
+          b = blobs + off[mi];
           const uint32_t L = len[mi];
+          bend = b + L;
           TxLayout t;
           tx_blob_parse(b, L, t);
           status[mi] = (uint8_t)t.status;
@@ -296,6 +428,7 @@ __global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restri
             sq[3] = make_uint4(sgw[12], sgw[13], sgw[14], sgw[15]);
             st8(pk + 32 * (size_t)mi, pkw);
             ss.init(b, L, kPrefixTxSign, &t);
+            nb = ss.blocks();
             phase = 0;
           } else {
             const uint4 z = make_uint4(0u, 0u, 0u, 0u), f = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -304,7 +437,8 @@ __global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restri
             pq[0] = z; pq[1] = z;
             uint4* mq = reinterpret_cast<uint4*>(msg + 32 * (size_t)mi);
             mq[0] = z; mq[1] = z;
-            ss.init(b, L, kPrefixTxId, nullptr);
+            bs.init(b - 4, L + 4);
+            nb = bs.blocks();
             phase = 1;
           }
           if (t.status == kTxDeferred || (phase == 1 && txid == nullptr)) {
@@ -314,7 +448,6 @@ __global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restri
               tq[1] = make_uint4(0u, 0u, 0u, 0u);
             }
           } else {
-            nb = ss.blocks();
             blk = 0;
             sha512_init(st);
             active = true;
@@ -323,9 +456,20 @@ __global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restri
       }
     }
     if (!__any(active)) break;
+    const uintptr_t blk_addr = (uintptr_t)(bs.q + 32 * blk);
+    const uintptr_t wsrc = phase == 0 ? (uintptr_t)ss.cursor() : blk_addr;
+    const uintptr_t wbase = active ? (wsrc & ~(uintptr_t)15) : 0;
+    wave_window_fill(win, wbase, (uintptr_t)b, (uintptr_t)bend, lane);
     if (active) {
+      const uint32_t* lw = reinterpret_cast<const uint32_t*>(win) + lane * (kWinBytes / 4);
       uint64_t w[16];
-      ss.block(w, blk, blk + 1 == nb);
+      if (phase == 0) {
+        const WinSrc src{lw, wbase, nullptr};
+        ss.block(w, blk, blk + 1 == nb, src);
+      } else {
+        block_from_window(w, lw, (uint32_t)(blk_addr & 15u) >> 2, bs.mis, (int32_t)bs.len - (int32_t)(128 * blk),
+                          blk + 1 == nb, bs.len, blk == 0, true, txn_le);
+      }
       sha512_compress(st, w);
       if (++blk == nb) {
         uint32_t h[8];
@@ -337,9 +481,8 @@ __global__ __launch_bounds__(kBlock) void tx_blob_kernel(const uint8_t* __restri
         if (phase == 0) {
           st8(msg + 32 * (size_t)mi, h);
           if (txid != nullptr) {
-            const uint8_t* b = blobs + off[mi];
-            ss.init(b, len[mi], kPrefixTxId, nullptr);
-            nb = ss.blocks();
+            bs.init(b - 4, len[mi] + 4);
+            nb = bs.blocks();
             blk = 0;
             sha512_init(st);
             phase = 1;
@@ -463,26 +606,42 @@ hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t*
   return hipGetLastError();
 }
 
+// queue workspace: [0] counter, [64..127] bucket counts, [128..191] cursors,
+// [256..) the order (n words)
+static hipError_t launch_order(const uint32_t* len, uint32_t n, uint32_t extra, uint32_t* qws, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(qws, 0, kQueueHeaderBytes, stream);
+  if (e != hipSuccess) return e;
+  uint32_t* hist = qws + 64;
+  uint32_t* cursor = qws + 128;
+  uint32_t* order = qws + kQueueHeaderBytes / 4;
+  const uint32_t tiles = (n + kBlock - 1) / kBlock;
+  const uint32_t grid = tiles < 1024u ? tiles : 1024u;
+  hipLaunchKernelGGL(order_count_kernel, dim3(grid), dim3(kBlock), 0, stream, len, n, extra, hist);
+  hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(64), 0, stream, hist, cursor);
+  hipLaunchKernelGGL(order_scatter_kernel, dim3(grid), dim3(kBlock), 0, stream, len, n, extra, cursor, order);
+  return hipGetLastError();
+}
+
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          uint32_t* counter, uint32_t grid, hipStream_t stream) {
+                          uint32_t* qws, uint32_t grid, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), stream);
+  hipError_t e = launch_order(len, n, 0u, qws, stream);
   if (e != hipSuccess) return e;
   const uint32_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(tx_hash_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, pre, off, len, n,
-                     msg, counter);
+                     msg, qws, qws + kQueueHeaderBytes / 4);
   return hipGetLastError();
 }
 
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* counter, uint32_t grid,
+                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
                           hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), stream);
+  hipError_t e = launch_order(len, n, 4u, qws, stream);
   if (e != hipSuccess) return e;
   const uint32_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(tx_blob_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, blobs, off, len,
-                     n, msg, sig, pk, txid, status, counter);
+                     n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4);
   return hipGetLastError();
 }
 

@@ -49,31 +49,108 @@ STL_HD void sha512_init(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
 }
 
+// ---- 64-bit words as 32-bit halves ----
+// gfx950 runs 64-bit shifts and adds (v_lshrrev_b64, v_lshl_add_u64) at a
+// fraction of the 32-bit rate; a rotate is two v_alignbit_b32, an add is
+// v_add_co_u32 + v_addc_co_u32, and three-way xors fuse into v_xor3_b32.
+struct W64 {
+  uint32_t lo, hi;
+};
+
+STL_HD W64 w64(uint64_t v) { return W64{(uint32_t)v, (uint32_t)(v >> 32)}; }
+STL_HD uint64_t u64(W64 v) { return ((uint64_t)v.hi << 32) | v.lo; }
+
+STL_HD uint32_t abit(uint32_t hi, uint32_t lo, uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (n & 31));
+#endif
+}
+
+template <int N>
+STL_HD W64 rotr(W64 x) {
+  static_assert(N > 0 && N < 64 && N != 32, "rotate");
+  if (N < 32) return W64{abit(x.hi, x.lo, N), abit(x.lo, x.hi, N)};
+  return W64{abit(x.lo, x.hi, N - 32), abit(x.hi, x.lo, N - 32)};
+}
+
+template <int N>
+STL_HD W64 shr(W64 x) {
+  static_assert(N > 0 && N < 32, "shift");
+  return W64{abit(x.hi, x.lo, N), x.hi >> N};
+}
+
+STL_HD W64 xor3(W64 a, W64 b, W64 c) { return W64{a.lo ^ b.lo ^ c.lo, a.hi ^ b.hi ^ c.hi}; }
+
+STL_HD W64 add(W64 a, W64 b) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(STL_SHA_ADD64)
+  return w64(u64(a) + u64(b));
+#endif
+  unsigned c;
+  const uint32_t lo = __builtin_addc(a.lo, b.lo, 0u, &c);
+  const uint32_t hi = __builtin_addc(a.hi, b.hi, c, &c);
+  return W64{lo, hi};
+}
+
+// (e & f) ^ (~e & g): v_bfi_b32 per half
+STL_HD W64 ch(W64 e, W64 f, W64 g) { return W64{(e.lo & f.lo) | (~e.lo & g.lo), (e.hi & f.hi) | (~e.hi & g.hi)}; }
+// majority = bfi(a ^ b, c, b)
+STL_HD W64 maj(W64 a, W64 b, W64 c) {
+  const uint32_t xl = a.lo ^ b.lo, xh = a.hi ^ b.hi;
+  return W64{(xl & c.lo) | (~xl & b.lo), (xh & c.hi) | (~xh & b.hi)};
+}
+
+// Round constant, pinned per round as a scalar pair (see the loop below).
+STL_HD W64 sha_kw(int i) {
+  W64 k = w64(sha_k(i));
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(k.lo), "+s"(k.hi));
+#endif
+  return k;
+}
+
 // One compression; w[16] = the block as big-endian 64-bit words (clobbered).
-STL_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
-  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+STL_HD void sha512_compress(uint64_t st[8], uint64_t w64in[16]) {
+  W64 w[16];
 #pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = w64(w64in[j]);
+  W64 a = w64(st[0]), b = w64(st[1]), c = w64(st[2]), d = w64(st[3]);
+  W64 e = w64(st[4]), f = w64(st[5]), g = w64(st[6]), h = w64(st[7]);
+#pragma clang loop unroll(full)
   for (int i = 0; i < 80; ++i) {
-    uint64_t wi;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Pin round i's message-schedule inputs behind round i-1's state, so the
+    // compiler cannot compute all 64 expansions up front (that keeps 80 words
+    // = 160 VGPRs live and caps occupancy at 2 waves per SIMD).
+    if (i >= 16) {
+      asm volatile("" : "+v"(a.lo), "+v"(e.lo), "+v"(w[(i - 15) & 15].lo), "+v"(w[(i - 15) & 15].hi),
+                   "+v"(w[(i - 2) & 15].lo), "+v"(w[(i - 2) & 15].hi));
+    }
+#endif
+    W64 wi;
     if (i < 16) {
       wi = w[i];
     } else {
-      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint64_t s0 = sha_ror(w15, 1) ^ sha_ror(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = sha_ror(w2, 19) ^ sha_ror(w2, 61) ^ (w2 >> 6);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+      const W64 w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      const W64 s0 = xor3(rotr<1>(w15), rotr<8>(w15), shr<7>(w15));
+      const W64 s1 = xor3(rotr<19>(w2), rotr<61>(w2), shr<6>(w2));
+      wi = add(add(w[i & 15], s0), add(w[(i - 7) & 15], s1));
       w[i & 15] = wi;
     }
-    const uint64_t S1 = sha_ror(e, 14) ^ sha_ror(e, 18) ^ sha_ror(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = h + S1 + ch + sha_k(i) + wi;
-    const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
-    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
-    STL_FE_FENCE();  // one round per scheduling region: bounds register pressure
+    const W64 S1 = xor3(rotr<14>(e), rotr<18>(e), rotr<41>(e));
+    const W64 t1 = add(add(h, S1), add(add(ch(e, f, g), sha_kw(i)), wi));
+    const W64 S0 = xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a));
+    const W64 t2 = add(S0, maj(a, b, c));
+    h = g; g = f; f = e; e = add(d, t1); d = c; c = b; b = a; a = add(t1, t2);
+#ifdef STL_SHA_FENCE
+    STL_FE_FENCE();
+#endif
   }
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+  st[0] = u64(add(w64(st[0]), a)); st[1] = u64(add(w64(st[1]), b));
+  st[2] = u64(add(w64(st[2]), c)); st[3] = u64(add(w64(st[3]), d));
+  st[4] = u64(add(w64(st[4]), e)); st[5] = u64(add(w64(st[5]), f));
+  st[6] = u64(add(w64(st[6]), g)); st[7] = u64(add(w64(st[7]), h));
 }
 
 STL_HD uint32_t bswap32(uint32_t x) {
@@ -182,16 +259,23 @@ struct ByteStream {
     for (uint32_t t = 0; t < valid; ++t) v |= (uint32_t)b[t] << (8 * t);
     return v;
   }
+  // aligned dword idx through a source that may serve it from a cache (the
+  // kernels' LDS window); Src(addr_of_dword, idx) falls back to dword(idx)
+  struct Direct {
+    const ByteStream* s;
+    STL_HD uint32_t operator()(uint32_t idx) const { return s->dword(idx); }
+  };
   // block blk as 16 big-endian words with the FIPS 180-4 padding applied
   // (0x80 after the message, zeros, 128-bit length in the final block)
-  STL_HD void block(uint64_t w[16], uint32_t blk, bool last) const {
-    uint32_t prev = dword(32 * blk);
+  template <typename Src>
+  STL_HD void block(uint64_t w[16], uint32_t blk, bool last, const Src& src) const {
+    uint32_t prev = src(32 * blk);
 #pragma unroll
     for (int j = 0; j < 32; j += 2) {
       uint32_t m[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const uint32_t next = dword(32 * blk + j + h + 1);
+        const uint32_t next = src(32 * blk + j + h + 1);
         uint32_t v = align_byte(next, prev, mis);
         prev = next;
         const int64_t keep = (int64_t)len - (int64_t)(128 * blk + 4 * (j + h));
@@ -208,8 +292,40 @@ struct ByteStream {
       w[15] = (uint64_t)len * 8;
     }
   }
+  STL_HD void block(uint64_t w[16], uint32_t blk, bool last) const { block(w, blk, last, Direct{this}); }
   STL_HD uint32_t blocks() const { return (len + 17 + 127) / 128; }
 };
+
+// Block assembly from a 36-word window: win[d4 .. d4+32] are the aligned
+// dwords 32*blk .. 32*blk+32 of a ByteStream (the kernels fill the window by
+// wave-cooperative 16-byte loads; d4 = that dword's offset in its 16-byte
+// granule).  rem = message bytes left at the block start (may be <= 0 in a
+// padding-only block).  With `prefix`, the message is a 4-byte prefix
+// followed by the stream's bytes shifted by 4: the caller built the stream 4
+// bytes before the data, and word 0 of block 0 is replaced by the prefix.
+STL_HD void block_from_window(uint64_t w[16], const uint32_t* win, uint32_t d4, uint32_t mis, int32_t rem,
+                              bool last, uint32_t total, bool first, bool has_prefix, uint32_t prefix_le) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t m[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = 2 * j + h;
+      uint32_t v = align_byte(win[d4 + i + 1], win[d4 + i], mis);
+      if (i == 0 && has_prefix && first) v = prefix_le;
+      const int32_t k = rem - 4 * i;  // message bytes from this word on
+      const int32_t kc = k < 0 ? 0 : (k > 4 ? 4 : k);
+      const uint32_t keep = kc == 4 ? 0xffffffffu : ((1u << (8 * kc)) - 1u);
+      const uint32_t pad = (k >= 0 && k < 4) ? (0x80u << (8 * kc)) : 0u;
+      m[h] = (v & keep) | pad;
+    }
+    w[j] = be64_from_le32(m[0], m[1]);
+  }
+  if (last) {
+    w[14] = 0;
+    w[15] = (uint64_t)total * 8u;
+  }
+}
 
 // SHA512Half(bytes) -> 8 little-endian words (the first 32 digest bytes)
 STL_HD void sha512_half_words(uint32_t out[8], const uint8_t* p, uint32_t len) {

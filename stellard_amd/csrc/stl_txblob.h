@@ -283,7 +283,12 @@ struct SpliceStream {
     nb = 4;
     done = false;
   }
-  STL_HD void fetch() {
+  // plain global (or host) load of the aligned dword at a
+  struct Direct {
+    STL_HD uint32_t operator()(const uint8_t* a) const { return *reinterpret_cast<const uint32_t*>(a); }
+  };
+  template <typename Src>
+  STL_HD void fetch(const Src& src) {
     while (pos == xs0 && pos < len) {
       pos = xe0;
       xs0 = xs1; xe0 = xe1;
@@ -300,8 +305,8 @@ struct SpliceStream {
     if (k > lim - pos) k = lim - pos;
     uint32_t v;
     if (pos >= sh && pos - sh + 4u <= len) {
-      v = *reinterpret_cast<const uint32_t*>(b + pos - sh) >> (8u * sh);
-    } else {  // the blob's last partial dword, byte by byte
+      v = src(b + pos - sh) >> (8u * sh);
+    } else {  // the blob's first / last partial dword, byte by byte
       v = 0;
       for (uint32_t i = 0; i < k; ++i) v |= (uint32_t)b[pos + i] << (8u * i);
     }
@@ -310,8 +315,9 @@ struct SpliceStream {
     nb += k;
     pos += k;
   }
-  STL_HD uint32_t word() {
-    while (nb < 4 && !done) fetch();
+  template <typename Src>
+  STL_HD uint32_t word(const Src& src) {
+    while (nb < 4 && !done) fetch(src);
     const uint32_t w = (uint32_t)acc;
     acc >>= 32;
     nb = nb >= 4 ? nb - 4 : 0;
@@ -319,13 +325,14 @@ struct SpliceStream {
   }
   STL_HD uint32_t blocks() const { return (total + 17u + 127u) / 128u; }
   // next 128-byte block (blocks are consumed in order) with FIPS 180-4 padding
-  STL_HD void block(uint64_t w[16], uint32_t blk, bool last) {
+  template <typename Src>
+  STL_HD void block(uint64_t w[16], uint32_t blk, bool last, const Src& src) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       uint32_t m[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        uint32_t v = word();
+        uint32_t v = word(src);
         const int64_t keep = (int64_t)total - (int64_t)(128u * blk + 4u * (2 * j + h));
         if (keep < 4) {
           v = keep <= 0 ? 0u : (v & ((1u << (8 * keep)) - 1u));
@@ -340,6 +347,10 @@ struct SpliceStream {
       w[15] = (uint64_t)total * 8u;
     }
   }
+  STL_HD void block(uint64_t w[16], uint32_t blk, bool last) { block(w, blk, last, Direct{}); }
+  // blob address of the next byte the stream will read (window placement)
+  STL_HD const uint8_t* cursor() const { return b + (pos == xs0 && pos < len ? xe0 : pos); }
+  STL_HD const uint8_t* end() const { return b + len; }
 };
 
 // n little-endian words from blob bytes [off, off + 4n) (off unaligned).

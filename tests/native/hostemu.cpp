@@ -135,6 +135,48 @@ void hostemu_tx_blob(const uint8_t* blob, uint32_t len, uint32_t* status, uint8_
   std::memcpy(layout, l, sizeof l);
 }
 
+// block_from_window (the hash kernels' assembly from an LDS window) against
+// ByteStream::block for a message at buf+off of length len: every block,
+// optionally with the 4-byte prefix form.  Returns the number of differing
+// blocks.  buf must have 16 readable bytes around the message.
+uint32_t hostemu_window_blocks(const uint8_t* buf, uint32_t off, uint32_t len, uint32_t prefix_le, int with_prefix) {
+  stl::ByteStream ref, bs;
+  uint32_t bad = 0;
+  if (with_prefix) {
+    // reference: the prefix and the message concatenated
+    std::vector<uint8_t> cat(4 + len + 4);
+    std::memcpy(cat.data(), &prefix_le, 4);
+    std::memcpy(cat.data() + 4, buf + off, len);
+    ref.init(cat.data(), len + 4);
+    bs.init(buf + off - 4, len + 4);
+    const uint32_t nb = ref.blocks();
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+      uint64_t a[16], b[16];
+      ref.block(a, blk, blk + 1 == nb);
+      const uintptr_t addr = (uintptr_t)(bs.q + 32 * blk), base = addr & ~(uintptr_t)15;
+      uint32_t win[36];
+      std::memcpy(win, (const void*)base, sizeof win);
+      stl::block_from_window(b, win, (uint32_t)(addr & 15u) >> 2, bs.mis, (int32_t)bs.len - (int32_t)(128 * blk),
+                             blk + 1 == nb, bs.len, blk == 0, true, prefix_le);
+      bad += std::memcmp(a, b, sizeof a) != 0;
+    }
+    return bad;
+  }
+  ref.init(buf + off, len);
+  const uint32_t nb = ref.blocks();
+  for (uint32_t blk = 0; blk < nb; ++blk) {
+    uint64_t a[16], b[16];
+    ref.block(a, blk, blk + 1 == nb);
+    const uintptr_t addr = (uintptr_t)(ref.q + 32 * blk), base = addr & ~(uintptr_t)15;
+    uint32_t win[36];
+    std::memcpy(win, (const void*)base, sizeof win);
+    stl::block_from_window(b, win, (uint32_t)(addr & 15u) >> 2, ref.mis, (int32_t)len - (int32_t)(128 * blk),
+                           blk + 1 == nb, len, false, false, 0u);
+    bad += std::memcmp(a, b, sizeof a) != 0;
+  }
+  return bad;
+}
+
 // blob_words as the kernel uses it to gather pk / sig (unaligned source)
 void hostemu_blob_words(const uint8_t* blob, uint32_t off, uint32_t n, uint32_t len, uint32_t* out) {
   stl::blob_words(out, blob, off, n, len);

@@ -40,3 +40,24 @@ def test_config5_lengths(emu):
         n = int(np.exp(rng.uniform(np.log(100), np.log(4096))))
         off = int(rng.integers(0, buf.size - n))
         assert _half(emu, buf, off, n) == hashlib.sha512(buf[off:off + n].tobytes()).digest()[:32]
+
+
+def test_block_from_window_matches_bytestream():
+    """The hash kernels assemble each SHA-512 block from a 144-byte LDS window
+    (block_from_window); on the host the same function must give ByteStream's
+    blocks at every alignment and length, with and without the 4-byte prefix
+    (the transaction-ID form "TXN\\0" || blob)."""
+    import ctypes
+
+    import numpy as np
+
+    from tests.oracle_bind import load_hostemu
+    emu = load_hostemu()
+    rng = np.random.default_rng(9)
+    buf = np.frombuffer(rng.bytes(6000), np.uint8).copy()
+    base = buf.ctypes.data
+    start = (16 - base % 16) % 16 + 32  # 16-byte aligned origin with room on both sides
+    for off in range(start, start + 16):
+        for ln in (0, 1, 3, 4, 5, 107, 108, 111, 112, 113, 127, 128, 129, 240, 256, 1000, 4100):
+            assert emu.hostemu_window_blocks(buf.ctypes.data_as(ctypes.c_void_p), off, ln, 0, 0) == 0, (off, ln)
+            assert emu.hostemu_window_blocks(buf.ctypes.data_as(ctypes.c_void_p), off, ln, 0x004E5854, 1) == 0, (off, ln)

@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Timing harness for the hashing kernels on config-5-shaped data (1,048,576
+transactions, blob lengths log-uniform in 100 B - 4 KB):
+
+  tx_hash   stl_tx_hash_batch_device over signing preimages
+  tx_blob   stl_tx_blob_prepare_device over whole serialized transactions
+            (canonical pass + signing hash + transaction ID)
+
+Signatures are random bytes (the hashing kernels do not verify).  Prints one
+JSON line; used for A/B runs and under rocprofv3.
+  python3 tools/hash_bench.py [--n N] [--reps R] [--no-ids]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def make_blobs(n, seed, uniform=0):
+    """Payment-shaped blobs: fixed fields, a MemoData pad to the target length
+    (log-uniform 100 B - 4 KB, or all `uniform` bytes)."""
+    rng = np.random.default_rng(seed)
+    target = np.exp(rng.uniform(np.log(100), np.log(4096), n)).astype(np.int64)
+    if uniform:
+        target[:] = uniform
+    head = (b"\x12\x00\x00" + b"\x22\x80\x00\x00\x00" + b"\x24\x00\x00\x00\x01" +
+            b"\x61" + (123456 | 0x4000000000000000).to_bytes(8, "big") +
+            b"\x68" + (10 | 0x4000000000000000).to_bytes(8, "big"))
+    rand = rng.bytes(n * 64 + 4096 * 4)
+    pres, blobs = [], []
+    for i in range(n):
+        r = rand[64 * i:64 * i + 64]
+        pk = r[:32]
+        tail = b"\x81\x14" + r[32:52] + b"\x83\x14" + r[44:64]
+        body = head + b"\x73\x20" + pk
+        pad = int(target[i]) - (len(body) + len(tail) + 66)
+        memo = b""
+        if pad > 3:
+            m = min(pad - 3, 12480)
+            if m <= 192:
+                memo = b"\x7d" + bytes([m]) + rand[i % 4096:i % 4096 + m]
+            else:
+                v = m - 193
+                memo = b"\x7d" + bytes([193 + (v >> 8), v & 0xFF]) + rand[i % 4096:i % 4096 + m]
+        sig = rand[(64 * i + 7) % (64 * n): (64 * i + 7) % (64 * n) + 64].ljust(64, b"\1")
+        pres.append(b"STX\x00" + body + memo + tail)
+        blobs.append(body + b"\x74\x40" + sig + memo + tail)
+    return pres, blobs
+
+
+def pack(chunks):
+    lens = np.array([len(c) for c in chunks], np.uint32)
+    offs = np.zeros(len(chunks), np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(chunks) + b"\0" * 4, np.uint8).copy()
+    return buf, offs, lens
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-ids", action="store_true")
+    ap.add_argument("--uniform", type=int, default=0, help="all blobs this many bytes")
+    args = ap.parse_args()
+    import ctypes
+
+    import torch
+    from stellard_amd import _native as N
+    from stellard_amd import verify as V
+    V.init(device_count=1)
+    n = args.n
+    pres, blobs = make_blobs(n, 0x5EED0005, args.uniform)
+    out = {"n": n}
+    s = torch.cuda.current_stream()
+    for name, chunks in (("tx_hash", pres), ("tx_blob", blobs)):
+        buf, offs, lens = pack(chunks)
+        d_buf = torch.from_numpy(buf).cuda()
+        d_off = torch.from_numpy(offs.view(np.int64)).cuda()
+        d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+        d_msg = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+
+        def run():
+            if name == "tx_hash":
+                N.check(N.load().stl_tx_hash_batch_device(
+                    ctypes.c_void_p(d_buf.data_ptr()), ctypes.c_void_p(d_off.data_ptr()),
+                    ctypes.c_void_p(d_len.data_ptr()), n, ctypes.c_void_p(d_msg.data_ptr()),
+                    ctypes.c_void_p(s.cuda_stream)), "tx_hash")
+                return None
+            return V.tx_blob_prepare_device(d_buf, d_off, d_len, tx_ids=not args.no_ids, stream=s)
+
+        o = run()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            run()
+            b.record(s)
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        ms = float(np.median(ts))
+        blocks = int(((lens.astype(np.int64) + (0 if name == "tx_hash" else 4) + 17 + 127) // 128).sum())
+        if name == "tx_blob" and not args.no_ids:
+            blocks *= 2  # signing hash + transaction ID (same length within 70 bytes)
+        out[name] = {"ms": ms, "tx_per_s": n / ms * 1e3, "bytes": int(lens.sum()),
+                     "GB_per_s": float(lens.sum()) / ms / 1e6, "sha512_blocks": blocks,
+                     "blocks_per_s": blocks / ms * 1e3}
+        if o is not None:
+            st = o["status"].cpu().numpy()
+            out[name]["status_counts"] = {str(k): int((st == k).sum()) for k in (0, 1, 2)}
+            if name == "tx_blob":
+                import hashlib
+                m = o["msg"].cpu().numpy()
+                for i in (0, n // 2, n - 1):
+                    assert bytes(m[i]) == hashlib.sha512(pres[i]).digest()[:32]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -146,8 +146,9 @@ def payment_preimages(pks, n, rng, pad_lens=None):
         if rng.random() < 0.8:
             amt = int(rng.integers(1, 10**11)) | 0x4000000000000000
             f += b"\x61" + amt.to_bytes(8, "big")              # Amount, native
-        else:
-            f += b"\x61" + rng.bytes(48)                       # Amount, IOU
+        else:                                                  # Amount, IOU (STAmount.cpp:465-488)
+            head = int(rng.integers(10**15, 10**16)) | ((int(rng.integers(-96, 81)) + 512 + 256 + 97) << 54)
+            f += b"\x61" + head.to_bytes(8, "big") + b"\0" * 12 + b"USD" + b"\0" * 5 + rng.bytes(20)
         f += b"\x68" + (10 | 0x4000000000000000).to_bytes(8, "big")  # Fee
         f += b"\x73\x20" + pks[a].tobytes()                    # SigningPubKey
         if pad_lens is not None:
@@ -297,8 +298,15 @@ def blob_leg(gpu, cpu, blobs, cpu_samples):
         b.record(gpu.stream)
         t.cuda.synchronize()
         ptimes.append(a.elapsed_time(b) * 1e-3)
-    gpu.V.tx_blob_verify_batch(blobs[:1024])
-    (hbits, hst), host_s = timed(lambda: gpu.V.tx_blob_verify_batch(blobs))
+    # host API (PCIe-inclusive): one stl_tx_blob_verify_batch call on packed host buffers
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    hst = np.zeros(n, np.uint8)
+    B = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    call = lambda: gpu.N.check(gpu.N.load().stl_tx_blob_verify_batch(  # noqa: E731
+        B(buf), B(offs), B(lens), n, B(bm), B(hst), None, 0), "stl_tx_blob_verify_batch")
+    call()
+    _, host_s = timed(call)
+    hbits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
     ref_bits, ref_s = timed(lambda: cpu.tx_blob_verify(buf, offs, lens, 16))
 
     def run(lo, hi, threads):

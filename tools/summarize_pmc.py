@@ -10,13 +10,14 @@ import statistics
 import sys
 
 d = sys.argv[1]
+kfilter = sys.argv[2] if len(sys.argv) > 2 else "verify"
 res = {}
 for path in sorted(glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True)):
     variant = os.path.relpath(path, d).split(os.sep)[0]
     agg = {}
     for r in csv.DictReader(open(path)):
         kname = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if "verify" not in kname:
+        if kfilter not in kname:
             continue
         key = (kname, r["Dispatch_Id"], r["Counter_Name"])
         agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
