@@ -143,6 +143,34 @@ int stl_tx_blob_prepare_device(const uint8_t *d_blobs, const uint64_t *d_offset,
                                size_t n, uint8_t *d_msg, uint8_t *d_sig, uint8_t *d_pk, uint8_t *d_tx_id,
                                uint8_t *d_status, void *stream);
 
+/* ---- request aggregator ----
+ * stellard checks transactions one at a time on JobQueue workers
+ * (jtTRANSACTION: PeerImp.cpp:64-73, NetworkOPs.cpp:298-320) and has an unused
+ * batching hook, TxQueue::addEntryForSigCheck (TxQueue.h:32-33).  An
+ * aggregator takes single requests from any thread and runs them as device
+ * batches: a batch starts when max_batch requests are pending or the oldest
+ * has waited max_delay_us.  Each request completes through its callback, on
+ * the aggregator's worker thread, with one verdict: */
+#define STL_VERDICT_REJECT 0
+#define STL_VERDICT_ACCEPT 1
+#define STL_VERDICT_DEFER 2 /* serialized tx not decided on the device (STL_TX_DEFERRED) */
+/* or a negative STL_E* code: the batch failed, run your own check. */
+typedef void (*stl_verdict_fn)(void *ctx, int verdict);
+typedef struct stl_batcher stl_batcher;
+
+/* flags: policy bits as for the batch calls.  NULL on bad arguments. */
+stl_batcher *stl_batcher_create(uint32_t max_batch, uint32_t max_delay_us, uint32_t flags);
+/* RippleAddress::verifySignature(hash, sig) for one signature (copied). */
+int stl_batcher_submit(stl_batcher *b, const uint8_t *sig, const uint8_t *msg32, const uint8_t *pk,
+                       stl_verdict_fn fn, void *ctx);
+/* SerializedTransaction::checkSign for one serialized transaction (copied). */
+int stl_batcher_submit_tx(stl_batcher *b, const uint8_t *blob, size_t len, stl_verdict_fn fn, void *ctx);
+/* Returns when every request submitted before the call has completed. */
+void stl_batcher_flush(stl_batcher *b);
+void stl_batcher_stats(stl_batcher *b, uint64_t *submitted, uint64_t *completed, uint64_t *batches);
+/* Completes every pending request, then frees the aggregator. */
+void stl_batcher_destroy(stl_batcher *b);
+
 /* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;
  * EdKeyPair::setSeed, EdKeyPair.cpp:25-33): RFC 8032 keypair from a 32-byte
  * seed and a detached signature over a 32-byte message. */

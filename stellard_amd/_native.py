@@ -48,7 +48,16 @@ SYMBOLS = [
      [_U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, ctypes.c_uint32]),
     ("stl_tx_blob_prepare_device", ctypes.c_int,
      [_U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, _U8P, _U8P, _P]),
+    ("stl_batcher_create", ctypes.c_void_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    ("stl_batcher_submit", ctypes.c_int, [_P, _U8P, _U8P, _U8P, _P, _P]),
+    ("stl_batcher_submit_tx", ctypes.c_int, [_P, _U8P, ctypes.c_size_t, _P, _P]),
+    ("stl_batcher_flush", None, [_P]),
+    ("stl_batcher_stats", None, [_P, _P, _P, _P]),
+    ("stl_batcher_destroy", None, [_P]),
 ]
+
+VERDICT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
+STL_VERDICT_REJECT, STL_VERDICT_ACCEPT, STL_VERDICT_DEFER = 0, 1, 2
 
 
 class StlError(RuntimeError):

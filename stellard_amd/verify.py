@@ -247,6 +247,84 @@ def tx_blob_prepare_device(blobs, offsets, lengths, tx_ids=True, stream=None):
     return out
 
 
+class Batcher:
+    """stl_batcher (include/stl.h): single requests from any thread, run as
+    device batches by max_batch / max_delay_us; ``submit`` / ``submit_tx``
+    return a Future-like handle whose ``result()`` is the verdict
+    (VERDICT_ACCEPT / VERDICT_REJECT / VERDICT_DEFER or a negative STL_E*)."""
+
+    class Handle:
+        def __init__(self):
+            import threading
+            self._ev = threading.Event()
+            self.verdict = None
+
+        def result(self, timeout=None):
+            if not self._ev.wait(timeout):
+                raise TimeoutError("verdict not delivered")
+            return self.verdict
+
+    def __init__(self, max_batch=4096, max_delay_us=1000, policy=POLICY_SODIUM_1_0_18):
+        import threading
+        self._lib = N.load()
+        self._b = self._lib.stl_batcher_create(max_batch, max_delay_us, policy)
+        if not self._b:
+            raise ValueError("stl_batcher_create rejected its arguments")
+        self._live = {}
+        self._mu = threading.Lock()
+        self._next = 0
+
+        def done(ctx, verdict):
+            with self._mu:
+                h = self._live.pop(ctx)
+            h.verdict = verdict
+            h._ev.set()
+
+        self._cb = N.VERDICT_FN(done)  # kept alive with the aggregator
+
+    def _register(self):
+        h = Batcher.Handle()
+        with self._mu:
+            self._next += 1
+            key = self._next
+            self._live[key] = h
+        return key, h
+
+    def submit(self, sig, msg32, pk):
+        key, h = self._register()
+        N.check(self._lib.stl_batcher_submit(self._b, bytes(sig), bytes(msg32), bytes(pk), self._cb, key),
+                "stl_batcher_submit")
+        return h
+
+    def submit_tx(self, blob):
+        key, h = self._register()
+        blob = bytes(blob)
+        N.check(self._lib.stl_batcher_submit_tx(self._b, blob, len(blob), self._cb, key), "stl_batcher_submit_tx")
+        return h
+
+    def flush(self):
+        self._lib.stl_batcher_flush(self._b)
+
+    def stats(self):
+        v = [ctypes.c_uint64(0) for _ in range(3)]
+        self._lib.stl_batcher_stats(self._b, *[ctypes.byref(x) for x in v])
+        return {"submitted": v[0].value, "completed": v[1].value, "batches": v[2].value}
+
+    def close(self):
+        if self._b:
+            self._lib.stl_batcher_destroy(self._b)
+            self._b = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+VERDICT_REJECT, VERDICT_ACCEPT, VERDICT_DEFER = N.STL_VERDICT_REJECT, N.STL_VERDICT_ACCEPT, N.STL_VERDICT_DEFER
+
+
 def sign_batch_device(seed, msg, stream=None):
     """RFC 8032 keypair(seed) + detached signature over msg, on the GPU.
     seed (n,32), msg (n,32) uint8 CUDA tensors -> (pk (n,32), sig (n,64))."""

@@ -47,3 +47,45 @@ def test_no_cpu_verify_without_gpu():
     lib = _native.load()
     rc = lib.stl_ed25519_verify_detached(bytes(64), bytes(32), 32, bytes(32))
     assert rc == _native.STL_ENODEV
+
+
+def test_batcher_without_device_completes_every_request_with_an_error():
+    """The aggregator (f2) on a GPU-less box: every request completes exactly
+    once, with a negative error (the caller's fallback signal), never a
+    reject; batches respect max_batch; flush waits for all; threads may submit
+    concurrently."""
+    import threading
+
+    from stellard_amd import verify as V
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    with V.Batcher(max_batch=16, max_delay_us=200) as b:
+        handles = []
+        lock = threading.Lock()
+
+        def worker(k):
+            for i in range(40):
+                h = b.submit(bytes([k]) * 64, bytes([i]) * 32, bytes(32)) if i % 3 else b.submit_tx(bytes(200))
+                with lock:
+                    handles.append(h)
+
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        b.flush()
+        st = b.stats()
+        assert st["submitted"] == 160 and st["completed"] == 160
+        assert st["batches"] >= 160 // 16
+        for h in handles:
+            assert h.result(timeout=5) < 0
+
+
+def test_batcher_rejects_bad_arguments():
+    from stellard_amd import _native as N
+    lib = N.load()
+    assert not lib.stl_batcher_create(0, 100, 0)
+    assert not lib.stl_batcher_create(16, 100, 0x80)
+    assert lib.stl_batcher_submit(None, bytes(64), bytes(32), bytes(32), None, None) == N.STL_EINVAL

@@ -429,3 +429,40 @@ def test_tx_blob_config5_sizes(stl, oracle):
     assert (st == 0).all() and bits.all()
     for i in rng.choice(len(blobs), 500, replace=False):
         assert bytes(ids[i]) == T.tx_id(blobs[i])
+
+
+def test_batcher_verdicts(stl, oracle, golden):
+    """The request aggregator (f2): single requests from 4 threads, batched by
+    size and delay, give the same verdicts as the batch calls -- golden
+    signatures (every Appendix-B class) and serialized transactions (special
+    cases: accept / reject / defer)."""
+    import threading
+    from tests import txblob as T
+    sig, msg, pk = _golden_arrays(golden)
+    exp = golden["expected_sodium_1_0_18"].astype(bool)
+    cases = T.special_cases(oracle)
+    blobs = [b for _, b, _ in cases]
+    bits, st = stl.tx_blob_verify_batch(blobs)
+    with stl.Batcher(max_batch=256, max_delay_us=300) as b:
+        hs, ht = [None] * len(sig), [None] * len(blobs)
+
+        def worker(k):
+            for i in range(k, len(sig), 4):
+                hs[i] = b.submit(sig[i], msg[i], pk[i])
+            for i in range(k, len(blobs), 4):
+                ht[i] = b.submit_tx(blobs[i])
+
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        b.flush()
+        got = np.array([h.result(timeout=30) for h in hs])
+        assert np.array_equal(got == stl.VERDICT_ACCEPT, exp)
+        assert set(np.unique(got)) <= {stl.VERDICT_ACCEPT, stl.VERDICT_REJECT}
+        gt = np.array([h.result(timeout=30) for h in ht])
+        want = np.where(st == 1, stl.VERDICT_DEFER, np.where(bits, stl.VERDICT_ACCEPT, stl.VERDICT_REJECT))
+        assert np.array_equal(gt, want)
+        s = b.stats()
+        assert s["completed"] == len(sig) + len(blobs)
