@@ -54,7 +54,7 @@ struct Device {
   uint32_t grid = 0;  // resident workgroups for the verify kernel
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status;
+  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide;
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;  // tx-hash work counter
   std::mutex ws_mu;
@@ -83,6 +83,11 @@ int setup_device(Device& d) {
   if (per_cu < 1) per_cu = 1;
   d.grid = (uint32_t)(d.cus * per_cu);
   STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  // wide base tables for [e]B (7.3 MB), built once on the device
+  int rc = d.wide.ensure(stl::kWideTableBytes);
+  if (rc) return rc;
+  STL_TRY(stl::launch_wide_table(static_cast<uint4*>(d.wide.p), d.stream));
+  STL_TRY(hipStreamSynchronize(d.stream));
   return STL_OK;
 }
 
@@ -171,7 +176,8 @@ int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t
   }
   STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                              static_cast<uint8_t*>(d.pk.p), (uint32_t)n, static_cast<uint64_t*>(d.bitmap.p), policy,
-                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false, s));
+                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false,
+                             static_cast<const uint4*>(d.wide.p), s));
   std::vector<uint8_t> host_words(words * 8);
   STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
   STL_TRY(hipStreamSynchronize(s));
@@ -215,7 +221,8 @@ int run_blob_shard(Device& d, const uint8_t* blobs, const uint64_t* off, const u
                               static_cast<uint32_t*>(d.ctr.p), hash_grid(d), s));
   STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                              static_cast<uint8_t*>(d.pk.p), (uint32_t)n, static_cast<uint64_t*>(d.bitmap.p), policy,
-                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false, s));
+                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false,
+                             static_cast<const uint4*>(d.wide.p), s));
   std::vector<uint8_t> host_words(words * 8);
   STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
   if (status) STL_TRY(hipMemcpyAsync(status + lo, d.status.p, n, hipMemcpyDeviceToHost, s));
@@ -299,7 +306,7 @@ void stl_shutdown(void) {
     (void)hipSetDevice(d->ordinal);
     (void)hipStreamSynchronize(d->stream);
     for (DevBuf* b : {&d->ws, &d->sig, &d->msg, &d->pk, &d->bitmap, &d->pre, &d->off, &d->len, &d->ctr, &d->txid,
-                      &d->status})
+                      &d->status, &d->wide})
       b->release();
     for (auto& kv : d->stream_ws) kv.second->release();
     for (auto& kv : d->stream_ctr) kv.second->release();
@@ -398,7 +405,8 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
                                static_cast<uint8_t*>(d.pre.p), meta, meta + 1, 1, static_cast<uint8_t*>(d.msg.p), s));
   STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                              static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
-                             STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true, s));
+                             STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true,
+                             static_cast<const uint4*>(d.wide.p), s));
   uint64_t word = 0;
   STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
   STL_TRY(hipStreamSynchronize(s));
@@ -420,7 +428,7 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   uint4* ws = nullptr;
   if ((rc = stream_workspace(d, s, &ws))) return rc;
   STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(d, n), false, s));
+                             grid_for(d, n), false, static_cast<const uint4*>(d.wide.p), s));
   return STL_OK;
 }
 

@@ -26,7 +26,7 @@ inline uint32_t kernel_mode(uint32_t flags) { return (flags & 0x1u) | ((flags & 
 
 const void* kernel_verify_msg32();
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
-                         uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
+                         uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k, const uint4* wide,
                          hipStream_t stream);
 hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t* m, const uint64_t* moff,
                            const uint64_t* mlen, uint32_t n, uint8_t* k_out, hipStream_t stream);
@@ -41,6 +41,9 @@ hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
                           hipStream_t stream);
+// Wide base tables (stl_verify_core.h): 2 * 32769 rows of 28 words.
+constexpr size_t kWideTableBytes = 2ull * 32769 * 28 * 4;
+hipError_t launch_wide_table(uint4* out, hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
                        uint32_t grid, hipStream_t stream);
 

@@ -127,23 +127,64 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_pre_ker
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
 
+// Wide-table reader of the main kernel: each lane's two rows (7 x 16 B each)
+// go straight from L2 / the Infinity Cache into its wave's LDS stage by
+// global_load_lds, issued before the position's doublings -- the latency is
+// hidden and no VGPRs are held across the doublings (the kernel runs at
+// 246 of 256).  Stage layout [row][chunk][lane]: conflict-free reads.
+struct WideLds {
+  const uint4* gtab;  // 2 * kWideEntries rows of 7 uint4
+  uint4* stage;       // this wave's 2 * 7 * 64 uint4
+  uint32_t lane;
+  int d[2];
+  __device__ void prefetch(int d0, int d1) {
+    d[0] = d0;
+    d[1] = d1;
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const uint32_t a = (uint32_t)(d[w] < 0 ? -d[w] : d[w]);
+      const uint4* src = gtab + ((size_t)w * kWideEntries + a) * 7;
+#pragma unroll
+      for (int c = 0; c < 7; ++c)
+        __builtin_amdgcn_global_load_lds(src + c, (__attribute__((address_space(3))) void*)(stage + (w * 7 + c) * 64),
+                                         16, 0, 0);
+    }
+  }
+  __device__ void madd(ge_p1p1& t, const ge_p3& acc, int which) const {
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the rows have landed in LDS
+    ge_niels n;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&n);
+    static_assert(sizeof(ge_niels) == 27 * 4, "niels layout");
+    uint32_t row[28];
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+      const uint4 v = stage[(which * 7 + c) * 64 + lane];
+      row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 27; ++i) w[i] = row[i];
+    ge_niels_cneg(n, d[which] < 0);
+    ge_madd(t, acc, n);
+  }
+};
+
 // Phase 2: [e]B + [c](-A) + [d](-Q) == O; grid-strides over 256-signature
 // tiles of [base, base+cnt) so the per-lane table workspace is bounded by the
 // resident lanes; one ballot word per wave.
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
-    uint4* __restrict__ ws) {
-  __shared__ uint32_t sB[2 * kBaseTableWords];
-  stage_base_table(sB, 2);
+    uint4* __restrict__ ws, const uint4* __restrict__ wide) {
+  __shared__ uint4 wstage[kBlock / 64][2 * 7 * 64];
   uint4* slot = lane_slot(ws);
   const TableView tab1{slot, 1}, tab2{slot + kTableQuads, 1};
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  WideLds wl{wide, wstage[wave], lane, {0, 0}};
   for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
     const uint32_t t = tile + threadIdx.x;
     const bool live = t < cnt;
     HalfState h;
     ld_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
-    const bool ok = verify_phase2_half(h, tab1, tab2, sB) && live;
+    const bool ok = verify_phase2_half(h, tab1, tab2, wl) && live;
     const uint64_t word = __ballot(ok);
     const uint32_t wbase = tile + wave * 64;
     if (lane == 0 && wbase < cnt) bitmap[(base + wbase) >> 6] = word;
@@ -569,9 +610,27 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
 // ---- host-side launchers (called from stl_api.cpp) ----
 const void* kernel_verify_msg32() { return reinterpret_cast<const void*>(&verify_main_kernel); }
 
+// Wide base tables: one thread per row (stl_verify_core.h wide_entry).
+__global__ __launch_bounds__(kBlock) void wide_table_kernel(uint32_t* __restrict__ out) {
+  const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= 2 * kWideEntries) return;
+  const int which = r >= kWideEntries ? 1 : 0;
+  uint32_t row[28];
+  wide_entry(row, which, r - (uint32_t)which * kWideEntries, &kBaseNiels[0][0][0]);
+  uint4* q = reinterpret_cast<uint4*>(out + (size_t)r * kWideRowWords);
+#pragma unroll
+  for (int c = 0; c < 7; ++c) q[c] = make_uint4(row[4 * c], row[4 * c + 1], row[4 * c + 2], row[4 * c + 3]);
+}
+
+hipError_t launch_wide_table(uint4* out, hipStream_t stream) {
+  hipLaunchKernelGGL(wide_table_kernel, dim3((2 * kWideEntries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                     reinterpret_cast<uint32_t*>(out));
+  return hipGetLastError();
+}
+
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
-                         hipStream_t stream) {
+                         const uint4* wide, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   // ws = [per-lane slots: grid x kWsBytesPerBlock][HalfState x kPreChunk][fallback words]
   uint4* slots = ws;
@@ -588,7 +647,7 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     else
       hipLaunchKernelGGL(verify_pre_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
                          policy, pre, fb);
-    hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots);
+    hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
                          policy, fb, bitmap, slots);

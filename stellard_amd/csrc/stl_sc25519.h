@@ -136,6 +136,26 @@ STL_HD void sc_recode256(uint32_t packed[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-2^16 recoding of a scalar < 2^253 into 16 digits in
+// [-32768, 32767] (digit 15 in [0, 2^13]), packed as int16, 2 digits per word
+// (digit 2m+j in bits 16j..16j+15 of word m).  Drives the [e]B part of the
+// half-size check with the two 32769-entry wide base tables.
+STL_HD void sc_recode65536(uint32_t packed[8], const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int e = (int)((s[m] >> (16 * j)) & 0xffffu) + carry;
+      carry = (e + 32768) >> 16;
+      e -= carry << 16;
+      word |= ((uint32_t)e & 0xffffu) << (16 * j);
+    }
+    packed[m] = word;
+  }
+}
+
 // out = (a*b + c) mod L   (signing: S = r + k*a)
 STL_HD void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]) {
   uint32_t p[16];

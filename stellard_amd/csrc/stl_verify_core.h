@@ -298,7 +298,7 @@ STL_HD bool verify_full_with_k(const uint32_t R[8], const uint32_t S[8], const u
 //   tops       bits 0-7: positions needed (max over c, d; 33 for almost
 //              every lane), bit 16 ok (pre-checks, decodings, S < L),
 //              bit 17 fallback (full-length path)
-//   edig       signed radix-256 digits of e = d*S mod L (32 digits)
+//   edig       signed radix-2^16 digits of e = d*S mod L (16 digits)
 //   P1, P2     affine P1 = sign(c) ? A : -A,  P2 = sign(d) ? Q : -Q
 struct HalfState {
   uint32_t cdig[5], ddig[5];
@@ -350,7 +350,7 @@ STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t
   o.P2y = negQ.Y;
   const int cneed = sc_recode16_half(o.cdig, c);
   const int dneed = sc_recode16_half(o.ddig, d);
-  sc_recode256(o.edig, e);
+  sc_recode65536(o.edig, e);
   const int need = cneed > dneed ? cneed : dneed;
   o.tops = (uint32_t)need | (ok ? kHalfOk : 0u) | (ok && !half ? kHalfFallback : 0u);
   o.pad = 0;
@@ -376,12 +376,91 @@ STL_HD int half_positions(int need) {
 #endif
 }
 
-// [|c|]P1 + [|d|]P2 + [e]B == O ?  Joint Straus over P <= 40 nibble
-// positions (P wave-uniform): c, d in signed radix 16 (9-entry per-lane
-// tables), e in signed radix 256 with its low 16 digits on table 0 (j*B) and
-// high 16 on table 1 (j*2^128*B), both added at even positions i <= 30.
-STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const TableView& tab2,
-                               const uint32_t* btab) {
+// ---- wide base tables for [e]B ----
+// Two tables of j*B and j*2^128*B, j = 0..32768 (entry 0 the identity), in
+// affine Niels form (28 words, canonical limbs): e in signed radix 2^16 takes
+// 16 mixed adds (8 per table, one at every fourth nibble position) instead of
+// 32 with the 128-entry LDS tables.  7.3 MB per device, built once at init
+// (wide_entry) and read through L2 / the Infinity Cache.
+constexpr uint32_t kWideEntries = 32769;
+constexpr uint32_t kWideRowWords = 28;
+constexpr size_t kWideTableWords = 2ull * kWideEntries * kWideRowWords;
+
+// Row j of wide table `which` from the first entry (1*P) of the 128-entry
+// base table: [j]P by double-and-add, then affine and canonical.
+STL_HD void wide_entry(uint32_t row[28], int which, uint32_t j, const uint32_t* btab) {
+  ge_niels P;
+  load_base_niels(P, btab + which * kBaseTableWords, 1);
+  ge_p3 acc;
+  ge_p2 acc2;
+  ge_p1p1 t;
+  ge_p3_0(acc);
+  ge_p2_0(acc2);
+  for (int bit = 15; bit >= 0; --bit) {
+    ge_p2_dbl(t, acc2);
+    ge_p1p1_to_p3(acc, t);
+    if ((j >> bit) & 1u) {
+      ge_madd(t, acc, P);
+      ge_p1p1_to_p3(acc, t);
+    }
+    ge_p3_to_p2(acc2, acc);
+  }
+  if (j >> 16) {  // j = 65536 does not occur (j <= 32768); kept total for safety
+    ge_p3_0(acc);
+  }
+  fe zi, x, y, ypx, ymx, xy, xy2d, c2d;
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi);
+  fe_mul(y, acc.Y, zi);
+  fe_add(ypx, y, x);
+  fe_carry(ypx);
+  fe_sub(ymx, y, x);
+  fe_mul(xy, x, y);
+  fe_const_2d(c2d);
+  fe_mul(xy2d, xy, c2d);
+  uint32_t w[8];
+  fe canon[3];
+  fe_tobytes(w, ypx);
+  fe_frombytes(canon[0], w);
+  fe_tobytes(w, ymx);
+  fe_frombytes(canon[1], w);
+  fe_tobytes(w, xy2d);
+  fe_frombytes(canon[2], w);
+  for (int k = 0; k < 3; ++k)
+    for (int i = 0; i < 9; ++i) row[9 * k + i] = canon[k].v[i];
+  row[27] = 0;
+}
+
+// Wide-table reader of the host build: rows straight from memory.
+struct WideHost {
+  const uint32_t* tab;  // kWideTableWords
+  int d[2];
+  STL_HD void prefetch(int d0, int d1) {
+    d[0] = d0;
+    d[1] = d1;
+  }
+  STL_HD void madd(ge_p1p1& t, const ge_p3& acc, int which) const {
+    const int a = d[which] < 0 ? -d[which] : d[which];
+    const uint32_t* row = tab + ((size_t)which * kWideEntries + (uint32_t)a) * kWideRowWords;
+    ge_niels n;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      n.ypx.v[i] = row[i];
+      n.ymx.v[i] = row[9 + i];
+      n.xy2d.v[i] = row[18 + i];
+    }
+    ge_niels_cneg(n, d[which] < 0);
+    ge_madd(t, acc, n);
+  }
+};
+
+// Phase 2 of the half-size check: [e]B + [c](-A) + [d](-Q) == O.  Joint
+// Straus over the nibble positions of c and d (two per-lane 9-entry tables),
+// with e's 16 radix-2^16 digits added from the wide tables at every fourth
+// position.  `Wide` reads table rows (WideHost here; the kernel's stages
+// them in LDS by asynchronous loads issued before the doublings).
+template <typename Wide>
+STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const TableView& tab2, Wide& wide) {
   {
     ge_p3 P;
     affine_to_p3(P, p.P1x, p.P1y);
@@ -415,7 +494,7 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
         dd[m] = dd[m - 1];
       }
     }
-    if ((i & 7) == 6 && i < 32) {  // next 4 radix-256 digits of e, low and high halves
+    if ((i & 7) == 4 && i < 32) {  // next 2 radix-2^16 digits of e, low and high halves
       we0 = ed[3];
       we1 = ed[7];
 #pragma unroll
@@ -427,28 +506,33 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     const int dc = (int32_t)wc >> 28, dq = (int32_t)wd >> 28;
     wc <<= 4;
     wd <<= 4;
+    const bool bpos = (i & 3) == 0 && i < 32;  // wave-uniform
+    int de0 = 0, de1 = 0;
+    if (bpos) {
+      de0 = (i & 4) ? (int32_t)we0 >> 16 : (int32_t)(we0 << 16) >> 16;
+      de1 = (i & 4) ? (int32_t)we1 >> 16 : (int32_t)(we1 << 16) >> 16;
+    }
     if (i >= npos) continue;  // wave-uniform: digits above every lane's need are 0
-    // Issue this position's two table loads ahead of the doublings (~15k
-    // cycles of independent work per wave): their latency (L2 / Infinity
-    // Cache) is hidden instead of stalling the adds.
+    // Issue this position's table loads ahead of the doublings (~15k cycles
+    // of independent work per wave): their latency (L2 / Infinity Cache) is
+    // hidden instead of stalling the adds.
     ge_cached ca, cq;
     tab1.load(dc < 0 ? -dc : dc, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
+    if (bpos) wide.prefetch(de0, de1);
     if (i != npos - 1) dbl4(acc, acc2);
     ge_cached_cneg(ca, dc < 0);
     ge_add_cached(t, acc, ca);
     ge_p1p1_to_p3(acc, t);
     ge_cached_cneg(cq, dq < 0);
     ge_add_cached(t, acc, cq);
-    if ((i & 1) || i > 31) {
+    if (!bpos) {
       ge_p1p1_to_p2(acc2, t);
     } else {
       ge_p1p1_to_p3(acc, t);
-      madd_base_digit(t, acc, btab, (int32_t)we0 >> 24);
-      we0 <<= 8;
+      wide.madd(t, acc, 0);
       ge_p1p1_to_p3(acc, t);
-      madd_base_digit(t, acc, btab + kBaseTableWords, (int32_t)we1 >> 24);
-      we1 <<= 8;
+      wide.madd(t, acc, 1);
       ge_p1p1_to_p2(acc2, t);
     }
   }
@@ -459,24 +543,5 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
   return (p.tops & kHalfOk) != 0 && (p.tops & kHalfFallback) == 0 && id;
 }
 
-// Full check for one signature given k = H(R||A||M) mod L: the half-size path,
-// or the full-length path for the rare lanes whose lattice reduction does not
-// fit.  tab1/tab2 are two per-lane 9-entry tables; btab the two base tables.
-STL_HD bool verify_with_k(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t k[8],
-                          uint32_t policy, const TableView& tab1, const TableView& tab2, const uint32_t* btab) {
-  HalfState h;
-  verify_phase1_half(h, R, S, A, k, policy);
-  if (h.tops & kHalfFallback) return verify_full_with_k(R, S, A, k, policy, tab1, btab);
-  return verify_phase2_half(h, tab1, tab2, btab);
-}
-
-// Fixed 32-byte message (the stellard signing hash): k computed in-lane.
-STL_HD bool verify_msg32(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint32_t M[8],
-                         uint32_t policy, const TableView& tab1, const TableView& tab2, const uint32_t* btab) {
-  uint32_t h[16], k[8];
-  sha512_hram32(h, R, A, M);
-  sc_reduce64(k, h);
-  return verify_with_k(R, S, A, k, policy, tab1, tab2, btab);
-}
 
 }  // namespace stl

@@ -6,6 +6,8 @@
 #include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 static std::atomic<uint64_t> g_bound_viol{0};
@@ -47,6 +49,28 @@ static void hostemu_check_sub(const stl::fe& a, const stl::fe& b) {
 
 static void load8(uint32_t w[8], const uint8_t* p) { std::memcpy(w, p, 32); }
 
+// The wide base tables as the device builds them (wide_entry), built once per
+// process on 8 threads.
+static const uint32_t* wide_tables() {
+  static std::vector<uint32_t> tab;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    tab.resize(stl::kWideTableWords);
+    const uint32_t rows = 2 * stl::kWideEntries;
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < 8; ++t)
+      th.emplace_back([t, rows] {
+        for (uint32_t r = t; r < rows; r += 8) {
+          const int which = r >= stl::kWideEntries ? 1 : 0;
+          stl::wide_entry(&tab[(size_t)r * stl::kWideRowWords], which, r - (uint32_t)which * stl::kWideEntries,
+                          &stl::kBaseNielsHost[0][0][0]);
+        }
+      });
+    for (auto& x : th) x.join();
+  });
+  return tab.data();
+}
+
 extern "C" {
 
 // Bitmap out, LSB-first; returns number of bound violations observed.
@@ -78,7 +102,10 @@ uint64_t hostemu_verify_batch_mode(const uint8_t* sig, const uint8_t* msg, const
       const bool flagged = (hs.tops & stl::kHalfFallback) != 0;
       fb += flagged;
       if (flagged && mode == 0) ok = stl::verify_full_with_k(R, S, A, k, policy, t1, btab);
-      else ok = stl::verify_phase2_half(hs, t1, t2, btab);
+      else {
+        stl::WideHost wide{wide_tables(), {0, 0}};
+        ok = stl::verify_phase2_half(hs, t1, t2, wide);
+      }
     }
     if (ok) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
   }
@@ -175,6 +202,11 @@ uint32_t hostemu_window_blocks(const uint8_t* buf, uint32_t off, uint32_t len, u
     bad += std::memcmp(a, b, sizeof a) != 0;
   }
   return bad;
+}
+
+// Row j of wide table `which` (28 words) as the device init kernel writes it.
+void hostemu_wide_row(int which, uint32_t j, uint32_t out[28]) {
+  std::memcpy(out, wide_tables() + ((size_t)which * stl::kWideEntries + j) * stl::kWideRowWords, 28 * 4);
 }
 
 // blob_words as the kernel uses it to gather pk / sig (unaligned source)

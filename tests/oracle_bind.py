@@ -198,6 +198,7 @@ def load_hostemu():
     lib.hostemu_sha512_half.argtypes = [V, ctypes.c_uint32, V]
     lib.hostemu_tx_blob.argtypes = [V, ctypes.c_uint32, V, V, V, V]
     lib.hostemu_blob_words.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, V]
+    lib.hostemu_wide_row.argtypes = [ctypes.c_int, ctypes.c_uint32, V]
     lib.hostemu_window_blocks.restype = ctypes.c_uint32
     lib.hostemu_window_blocks.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
     return lib
