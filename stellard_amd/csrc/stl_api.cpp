@@ -52,7 +52,8 @@ struct Device {
   int ordinal = 0;
   int cus = 0;
   uint32_t grid = 0;  // resident workgroups for the verify kernel
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // kernels of the host batch API
+  hipStream_t copy = nullptr;    // its host-to-device copies (overlap the previous chunk's kernels)
   std::mutex mu;
   DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide;
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
@@ -83,6 +84,7 @@ int setup_device(Device& d) {
   if (per_cu < 1) per_cu = 1;
   d.grid = (uint32_t)(d.cus * per_cu);
   STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  STL_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
   // wide base tables for [e]B (7.3 MB), built once on the device
   int rc = d.wide.ensure(stl::kWideTableBytes);
   if (rc) return rc;
@@ -135,6 +137,66 @@ void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
   *hi = std::min(n, (size_t)(r + 1) * per * 64);
 }
 
+// ---- host batch API: chunked copy/compute pipeline ----
+// A shard is processed in chunks of kPipeChunk signatures (a multiple of 64,
+// so every chunk starts on a bitmap word).  Chunk c's inputs are copied on
+// d.copy while chunk c-1's kernels run on d.stream; an event orders each
+// chunk's kernels after its copy.  Device buffers hold the whole shard, so no
+// buffer is reused while a kernel may still read it.  Variable-length bytes
+// (preimages, blobs) are copied up to a watermark: chunk c copies
+// [watermark, max end of its rows), which is the whole contiguous range when
+// offsets ascend and stays correct for any order (rows below the watermark
+// were copied by an earlier chunk).
+constexpr size_t kPipeChunk = (size_t)1 << 18;
+
+struct Pipeline {
+  Device& d;
+  std::vector<hipEvent_t> ev;
+  explicit Pipeline(Device& dev) : d(dev) {}
+  ~Pipeline() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+  // Make d.stream wait for everything issued on d.copy so far.
+  int join_copy() {
+    hipEvent_t e;
+    STL_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev.push_back(e);
+    STL_TRY(hipEventRecord(e, d.copy));
+    STL_TRY(hipStreamWaitEvent(d.stream, e, 0));
+    return STL_OK;
+  }
+};
+
+// Rebased offsets of rows [lo, hi) and the byte range they span.
+int rebase(const uint64_t* off, const uint32_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff,
+           std::vector<uint64_t>& row_end, uint64_t* base_out, uint64_t* bytes_out) {
+  const size_t n = hi - lo;
+  const uint64_t base = off[lo];
+  uint64_t end = base;
+  roff.resize(n);
+  row_end.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (off[lo + i] < base) return STL_EINVAL;
+    roff[i] = off[lo + i] - base;
+    row_end[i] = roff[i] + len[lo + i];
+    end = std::max<uint64_t>(end, off[lo + i] + len[lo + i]);
+  }
+  *base_out = base;
+  *bytes_out = end - base;
+  return STL_OK;
+}
+
+// Copy the bytes rows [c0, c1) need that are not on the device yet.
+int copy_rows(Pipeline& pl, uint8_t* dst, const uint8_t* src, const std::vector<uint64_t>& row_end, size_t c0,
+              size_t c1, uint64_t* watermark) {
+  uint64_t need = *watermark;
+  for (size_t i = c0; i < c1; ++i) need = std::max(need, row_end[i]);
+  if (need > *watermark)
+    STL_TRY(hipMemcpyAsync(dst + *watermark, src + *watermark, need - *watermark, hipMemcpyHostToDevice, pl.d.copy));
+  *watermark = need;
+  return STL_OK;
+}
+
 // Verify one shard [lo, hi) on device d, synchronously; writes the host bitmap
 // bytes [lo/8, ceil(hi/8)).  msg32 == nullptr means tx mode (preimages).
 int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t* pk, const uint8_t* pre,
@@ -148,39 +210,41 @@ int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t
   if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(n * 64)) ||
       (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)))
     return rc;
-  hipStream_t s = d.stream;
-  STL_TRY(hipMemcpyAsync(d.sig.p, sig + 64 * lo, n * 64, hipMemcpyHostToDevice, s));
-  STL_TRY(hipMemcpyAsync(d.pk.p, pk + 32 * lo, n * 32, hipMemcpyHostToDevice, s));
-  if (msg32) {
-    STL_TRY(hipMemcpyAsync(d.msg.p, msg32 + 32 * lo, n * 32, hipMemcpyHostToDevice, s));
-  } else {
-    // tx mode: copy this shard's preimage bytes with offsets rebased to 0
-    const uint64_t base = off[lo];
-    uint64_t end = base;
-    std::vector<uint64_t> roff(n);
-    for (size_t i = 0; i < n; ++i) {
-      if (off[lo + i] < base) return STL_EINVAL;
-      roff[i] = off[lo + i] - base;
-      end = std::max<uint64_t>(end, off[lo + i] + len[lo + i]);
-    }
-    const size_t bytes = (size_t)(end - base);
+  std::vector<uint64_t> roff, row_end;
+  uint64_t base = 0, bytes = 0, mark = 0;
+  if (!msg32) {
+    if ((rc = rebase(off, len, lo, hi, roff, row_end, &base, &bytes))) return rc;
     if ((rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
-        (rc = d.ctr.ensure(stl::hash_queue_bytes(n))))
+        (rc = d.ctr.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk)))))
       return rc;
-    if (bytes) STL_TRY(hipMemcpyAsync(d.pre.p, pre + base, bytes, hipMemcpyHostToDevice, s));
-    STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, s));
-    STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, s));
-    STL_TRY(stl::launch_tx_hash(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p),
-                                static_cast<uint32_t*>(d.len.p), (uint32_t)n, static_cast<uint8_t*>(d.msg.p),
-                                static_cast<uint32_t*>(d.ctr.p), hash_grid(d), s));
+    STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, d.copy));
+    STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, d.copy));
   }
-  STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
-                             static_cast<uint8_t*>(d.pk.p), (uint32_t)n, static_cast<uint64_t*>(d.bitmap.p), policy,
-                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false,
-                             static_cast<const uint4*>(d.wide.p), s));
+  Pipeline pl(d);
+  uint8_t* dsig = static_cast<uint8_t*>(d.sig.p);
+  uint8_t* dmsg = static_cast<uint8_t*>(d.msg.p);
+  uint8_t* dpk = static_cast<uint8_t*>(d.pk.p);
+  for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
+    const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
+    STL_TRY(hipMemcpyAsync(dsig + 64 * c0, sig + 64 * (lo + c0), cn * 64, hipMemcpyHostToDevice, d.copy));
+    STL_TRY(hipMemcpyAsync(dpk + 32 * c0, pk + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
+    if (msg32) {
+      STL_TRY(hipMemcpyAsync(dmsg + 32 * c0, msg32 + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
+    } else if ((rc = copy_rows(pl, static_cast<uint8_t*>(d.pre.p), pre + base, row_end, c0, c1, &mark))) {
+      return rc;
+    }
+    if ((rc = pl.join_copy())) return rc;
+    if (!msg32)
+      STL_TRY(stl::launch_tx_hash(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p) + c0,
+                                  static_cast<uint32_t*>(d.len.p) + c0, (uint32_t)cn, dmsg + 32 * c0,
+                                  static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream));
+    STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
+                               static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, policy, static_cast<uint4*>(d.ws.p),
+                               grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream));
+  }
   std::vector<uint8_t> host_words(words * 8);
-  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
-  STL_TRY(hipStreamSynchronize(s));
+  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, d.stream));
+  STL_TRY(hipStreamSynchronize(d.stream));
   // lo is a multiple of 64, so the shard starts on a byte boundary
   std::memcpy(bitmap + lo / 8, host_words.data(), (n + 7) / 8);
   return STL_OK;
@@ -196,38 +260,40 @@ int run_blob_shard(Device& d, const uint8_t* blobs, const uint64_t* off, const u
   STL_TRY(hipSetDevice(d.ordinal));
   int rc;
   const size_t words = (n + 63) / 64;
-  const uint64_t base = off[lo];
-  uint64_t end = base;
-  std::vector<uint64_t> roff(n);
-  for (size_t i = 0; i < n; ++i) {
-    if (off[lo + i] < base) return STL_EINVAL;
-    roff[i] = off[lo + i] - base;
-    end = std::max<uint64_t>(end, off[lo + i] + len[lo + i]);
-  }
-  const size_t bytes = (size_t)(end - base);
+  std::vector<uint64_t> roff, row_end;
+  uint64_t base = 0, bytes = 0, mark = 0;
+  if ((rc = rebase(off, len, lo, hi, roff, row_end, &base, &bytes))) return rc;
   if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(n * 64)) ||
       (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)) ||
       (rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
-      (rc = d.ctr.ensure(stl::hash_queue_bytes(n))) || (rc = d.status.ensure(n)) || (txid && (rc = d.txid.ensure(n * 32))))
+      (rc = d.ctr.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk)))) || (rc = d.status.ensure(n)) ||
+      (txid && (rc = d.txid.ensure(n * 32))))
     return rc;
-  hipStream_t s = d.stream;
-  if (bytes) STL_TRY(hipMemcpyAsync(d.pre.p, blobs + base, bytes, hipMemcpyHostToDevice, s));
-  STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, s));
-  STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, s));
-  STL_TRY(stl::launch_tx_blob(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p),
-                              static_cast<uint32_t*>(d.len.p), (uint32_t)n, static_cast<uint8_t*>(d.msg.p),
-                              static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.pk.p),
-                              txid ? static_cast<uint8_t*>(d.txid.p) : nullptr, static_cast<uint8_t*>(d.status.p),
-                              static_cast<uint32_t*>(d.ctr.p), hash_grid(d), s));
-  STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
-                             static_cast<uint8_t*>(d.pk.p), (uint32_t)n, static_cast<uint64_t*>(d.bitmap.p), policy,
-                             static_cast<uint4*>(d.ws.p), grid_for(d, n), false,
-                             static_cast<const uint4*>(d.wide.p), s));
+  Pipeline pl(d);
+  STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, d.copy));
+  STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, d.copy));
+  uint8_t* dsig = static_cast<uint8_t*>(d.sig.p);
+  uint8_t* dmsg = static_cast<uint8_t*>(d.msg.p);
+  uint8_t* dpk = static_cast<uint8_t*>(d.pk.p);
+  uint8_t* dtxid = txid ? static_cast<uint8_t*>(d.txid.p) : nullptr;
+  for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
+    const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
+    if ((rc = copy_rows(pl, static_cast<uint8_t*>(d.pre.p), blobs + base, row_end, c0, c1, &mark))) return rc;
+    if ((rc = pl.join_copy())) return rc;
+    STL_TRY(stl::launch_tx_blob(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p) + c0,
+                                static_cast<uint32_t*>(d.len.p) + c0, (uint32_t)cn, dmsg + 32 * c0, dsig + 64 * c0,
+                                dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr,
+                                static_cast<uint8_t*>(d.status.p) + c0, static_cast<uint32_t*>(d.ctr.p),
+                                hash_grid(d), d.stream));
+    STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
+                               static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, policy, static_cast<uint4*>(d.ws.p),
+                               grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream));
+  }
   std::vector<uint8_t> host_words(words * 8);
-  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
-  if (status) STL_TRY(hipMemcpyAsync(status + lo, d.status.p, n, hipMemcpyDeviceToHost, s));
-  if (txid) STL_TRY(hipMemcpyAsync(txid + 32 * lo, d.txid.p, n * 32, hipMemcpyDeviceToHost, s));
-  STL_TRY(hipStreamSynchronize(s));
+  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, d.stream));
+  if (status) STL_TRY(hipMemcpyAsync(status + lo, d.status.p, n, hipMemcpyDeviceToHost, d.stream));
+  if (txid) STL_TRY(hipMemcpyAsync(txid + 32 * lo, d.txid.p, n * 32, hipMemcpyDeviceToHost, d.stream));
+  STL_TRY(hipStreamSynchronize(d.stream));
   std::memcpy(bitmap + lo / 8, host_words.data(), (n + 7) / 8);
   return STL_OK;
 }
@@ -310,7 +376,9 @@ void stl_shutdown(void) {
       b->release();
     for (auto& kv : d->stream_ws) kv.second->release();
     for (auto& kv : d->stream_ctr) kv.second->release();
+    (void)hipStreamSynchronize(d->copy);
     (void)hipStreamDestroy(d->stream);
+    (void)hipStreamDestroy(d->copy);
   }
   g_devs.clear();
   g_init = false;
