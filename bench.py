@@ -161,6 +161,14 @@ def main():
         if os.path.exists(tp):
             with open(tp) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
+        valu_busy = None
+        vp = os.path.join(ROOT, "profiles", "valu_latest.json")
+        if os.path.exists(vp):
+            with open(vp) as f:
+                vd = json.load(f)
+            valu_busy = {"launch_pct": vd.get("launch_valu_busy_pct"),
+                         "per_kernel_pct": {k: v.get("VALUBusy") for k, v in vd.get("kernels", {}).items()},
+                         "source": "rocprofv3 --pmc VALUBusy of this build, profiles/valu_latest.json"}
         line = {
             "metric": "Ed25519 tx verifies/sec",
             "value": value,
@@ -182,7 +190,8 @@ def main():
                          "kernel_ms": kern_ms, "work_per_verify": W_VERIFY,
                          "kernels": "verify_pre + verify_main + verify_fallback, one stream, HIP events around "
                                     "each stl_ed25519_verify_batch_device call",
-                         "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9)},
+                         "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9),
+                         "valu_busy_pmc": valu_busy},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

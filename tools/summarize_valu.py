@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Summarise tools/valu_pmc.sh output into profiles/valu_latest.json.
+
+Per verify kernel (mean over the profiled launches): VALUBusy and
+VALUUtilization (rocprofv3 derived metrics), OccupancyPercent, VALU
+instruction counts (SQ_INSTS_VALU / _INT32 / _INT64 / _IOPS) and the kernel's
+GPU-active cycles; plus the launch-level VALUBusy weighted by each kernel's
+GRBM_GUI_ACTIVE cycles.  usage: summarize_valu.py gpurun_out/<dir> [--out F]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+MEAN = {"VALUBusy", "VALUUtilization", "OccupancyPercent", "MeanOccupancyPerActiveCU"}
+
+
+def load(d):
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, "*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            if "verify" not in k:
+                continue
+            # one row per (dispatch, counter): sum over dimensions per dispatch
+            per[k][(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))
+    out = {}
+    for k, v in per.items():
+        acc = collections.defaultdict(list)
+        for (c, _), xs in v.items():
+            acc[c].append(sum(xs) / len(xs) if c in MEAN else sum(xs))
+        out[k] = {c: sum(xs) / len(xs) for c, xs in acc.items()}
+    return out
+
+
+def main():
+    d = sys.argv[1]
+    out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "valu_latest.json")
+    k = load(d)
+    w = sum(v.get("GRBM_GUI_ACTIVE", 0) for v in k.values())
+    busy = sum(v.get("VALUBusy", 0) * v.get("GRBM_GUI_ACTIVE", 0) for v in k.values()) / w if w else None
+    doc = {"source": d + " (rocprofv3 --pmc, one pass per counter group: tools/valu_pmc.sh)",
+           "launch_valu_busy_pct": busy, "kernels": k}
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
