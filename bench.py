@@ -188,7 +188,7 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
                          "kernel_ms": kern_ms, "work_per_verify": W_VERIFY,
-                         "kernels": "verify_pre + verify_main + verify_fallback, one stream, HIP events around "
+                         "kernels": "verify_scalar + verify_point + verify_main + verify_fallback, one stream, HIP events around "
                                     "each stl_ed25519_verify_batch_device call",
                          "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9),
                          "valu_busy_pmc": valu_busy},

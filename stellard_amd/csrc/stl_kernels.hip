@@ -1,9 +1,10 @@
 // stl_kernels.hip -- gfx950 kernels of libstl.
 //
-//   verify_pre_kernel     phase 1 of one Ed25519 verification per lane
+//   verify_scalar_kernel  phase 1a of one Ed25519 verification per lane
 //                         (RippleAddress::verifySignature over the 32-byte
-//                         signing hash, RippleAddress.cpp:190-200): pre-checks,
-//                         k, decompression of A and R, half-size scalars.
+//                         signing hash, RippleAddress.cpp:190-200): k,
+//                         half-size scalars (c, d), e, digits.
+//   verify_point_kernel   phase 1b: pre-checks, decompression of A and R.
 //   verify_main_kernel    phase 2, the hot loop: [e]B + [c](-A) + [d](-Q) == O,
 //                         accept bits assembled per wave with a 64-bit ballot.
 //   verify_fallback_kernel  full-length check for the rare flagged lanes.
@@ -31,6 +32,11 @@
 #endif
 #ifndef STL_PRE_WAVES_PER_SIMD
 #define STL_PRE_WAVES_PER_SIMD 2
+#endif
+// Scalar half of phase 1 (SHA-512 of k, lattice reduction): serial
+// dependency chains with few live registers, so occupancy hides latency.
+#ifndef STL_SCALAR_WAVES_PER_SIMD
+#define STL_SCALAR_WAVES_PER_SIMD 4
 #endif
 // Hash kernels: waves per SIMD (SHA-512 rounds are a serial chain per lane,
 // so occupancy hides the VALU and memory latency).
@@ -101,28 +107,57 @@ __device__ __forceinline__ void load_k(uint32_t k[8], const uint32_t R[8], const
   }
 }
 
-// Phase 1: one signature per lane -- pre-checks, k = SHA-512(R||A||M) mod L
-// (or k given, PRE_K), decompression of A and R, lattice reduction of k to
-// half-size (c, d), e = d*S mod L.  Signatures [base, base+cnt); one ballot
-// word of "needs the full-length path" flags per wave.
+// Phase 1a: one signature per lane -- k = SHA-512(R||A||M) mod L (or k
+// given, PRE_K), lattice reduction of k to half-size (c, d), e = d*S mod L,
+// digits.  Writes quads 0-4 of the lane's HalfState.  Signatures [base,
+// base+cnt).
 template <bool PRE_K>
-__global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_pre_kernel(const uint8_t* __restrict__ sig,
-                                                            const uint8_t* __restrict__ msg_or_k,
-                                                            const uint8_t* __restrict__ pk, uint32_t base,
-                                                            uint32_t cnt, uint32_t policy, uint4* __restrict__ pre,
-                                                            uint64_t* __restrict__ fb_words) {
+__global__ __launch_bounds__(kBlock, STL_SCALAR_WAVES_PER_SIMD) void verify_scalar_kernel(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
+    uint32_t base, uint32_t cnt, uint4* __restrict__ pre) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  const bool live = t < cnt;
-  const size_t j = (size_t)base + (live ? t : cnt - 1);
+  if (t >= cnt) return;  // no wave-level collective in this kernel
+  const size_t j = (size_t)base + t;
   uint32_t R[8], S[8], A[8], k[8];
   ld8(R, sig + 64 * j);
   ld8(S, sig + 64 * j + 32);
   ld8(A, pk + 32 * j);
   load_k(k, R, A, msg_or_k, j, PRE_K);
   HalfState h;
-  verify_phase1_half(h, R, S, A, k, policy & 1u);
+  verify_phase1_scalars(h, S, k);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
+  uint4* q = pre + (size_t)t * 14;
+#pragma unroll
+  for (int i = 0; i < kHalfScalarQuads; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Phase 1b: pre-checks, decompression of A and R, signed P1 / P2, final
+// flags (quad 2 rewritten, quads 5-13 written); one ballot word of "needs
+// the full-length path" flags per wave.
+__global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_point_kernel(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk, uint32_t base, uint32_t cnt, uint32_t policy,
+    uint4* __restrict__ pre, uint64_t* __restrict__ fb_words) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = t < cnt;
+  const uint32_t tt = live ? t : cnt - 1;
+  const size_t j = (size_t)base + tt;
+  uint32_t R[8], S[8], A[8];
+  ld8(R, sig + 64 * j);
+  ld8(S, sig + 64 * j + 32);
+  ld8(A, pk + 32 * j);
+  uint4* q = pre + (size_t)tt * 14;
+  HalfState h;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&h);
+  const uint4 q2 = q[kHalfTopsWord / 4];
+  w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+  static_assert(kHalfTopsWord == 10, "tops is word 2 of quad 2");
+  verify_phase1_points(h, R, S, A, policy & 1u);
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
-  if (live) st_words<14>(pre + (size_t)t * 14, h);
+  if (live) {
+    q[kHalfTopsWord / 4] = make_uint4(w[8], w[9], w[10], w[11]);
+#pragma unroll
+    for (int i = kHalfScalarQuads; i < 14; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  }
   const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
@@ -642,11 +677,10 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
     const dim3 g2(tiles < grid ? tiles : grid);
     if (pre_k)
-      hipLaunchKernelGGL(verify_pre_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
-                         pre, fb);
+      hipLaunchKernelGGL(verify_scalar_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     else
-      hipLaunchKernelGGL(verify_pre_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                         policy, pre, fb);
+      hipLaunchKernelGGL(verify_scalar_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
+    hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,

@@ -17,10 +17,13 @@
 //
 // (c, d) comes from the extended Euclidean algorithm on (8L, k), stopped when
 // the remainder drops below 2^128 (r_i == t_i * k mod 8L, |t_i| <= 8L/r_{i-1}),
-// then made odd in d by combining with the previous row.  Quotients are taken
-// from fp64 approximations and corrected exactly.  Any lane whose (c, d) does
-// fit the 158-bit budget, or needs a quotient >= 2^32, is flagged for the
-// full-length path (verify_full_with_k), which is exact for every input.
+// then made odd in d by combining with the previous row.  The Euclid runs as
+// Lehmer rounds (lat_lehmer_round): quotients from the leading 53 bits in
+// fp64, each certified to equal the full-precision quotient before it is
+// taken, so the row sequence is exactly the one-step-at-a-time Euclid's.  Any
+// lane whose (c, d) does not fit the 158-bit budget, or needs a quotient >=
+// 2^32, is flagged for the full-length path (verify_full_with_k), which is
+// exact for every input.
 #pragma once
 #include "stl_sc25519.h"
 
@@ -142,49 +145,216 @@ STL_HD void lat_step(uint32_t x[8], const uint32_t y[8], uint32_t tx[5], const u
 // 5-word magnitude < 2^kHalfBits
 STL_HD bool lat_fits(const uint32_t v[5]) { return (v[4] >> (kHalfBits - 128)) == 0; }
 
+// ---- Lehmer reduction (Knuth 4.5.2 Algorithm L with an exact certificate) ----
+// A round reads the leading 53 bits of both rows at one shift, runs Euclid
+// on those doubles while each quotient is PROVABLY the full rows' quotient,
+// then applies the accumulated 2x2 matrix to the full rows once.  The
+// sequence of rows is therefore exactly the one-quotient-per-step Euclid's
+// (tests/test_halfscalar.py::test_lattice_equals_exact_euclid), at a
+// fraction of the multi-word work.
+
+// wave-uniform loop control: any lane still active (device), this lane (host)
+STL_HD bool lat_any(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __any(b);
+#else
+  return b;
+#endif
+}
+
+// quotient estimate x / y (corrected exactly by the caller)
+STL_HD double lat_div_est(double x, double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return x * __builtin_amdgcn_rcp(y);
+#else
+  return x / y;
+#endif
+}
+
+// Leading parts at a common shift sh: x = floor(r1 / 2^sh) in [2^52, 2^53),
+// y = floor(r2 / 2^sh) (exact integers as doubles), and thr = 2^(128 - sh).
+// Requires r1 >= 2^128 and r2 < r1 for a meaningful result.
+STL_HD void lat_lead(double& x, double& y, double& thr, const uint32_t r1[8], const uint32_t r2[8]) {
+  const int t = r1[7] ? 7 : r1[6] ? 6 : r1[5] ? 5 : 4;
+  uint32_t a2 = 0, a1 = 0, a0 = 0, b2 = 0, b1 = 0, b0 = 0;
+#pragma unroll
+  for (int i = 4; i < 8; ++i) {
+    if (t == i) {
+      a2 = r1[i];
+      a1 = r1[i - 1];
+      a0 = r1[i - 2];
+      b2 = r2[i];
+      b1 = r2[i - 1];
+      b0 = r2[i - 2];
+    }
+  }
+  const int lz = a2 ? __builtin_clz(a2) : 0;
+  uint64_t ta = ((uint64_t)a2 << 32) | a1, tb = ((uint64_t)b2 << 32) | b1;
+  if (lz) {
+    ta = (ta << lz) | (a0 >> (32 - lz));
+    tb = (tb << lz) | (b0 >> (32 - lz));
+  }
+  x = (double)(ta >> 11);
+  y = (double)(tb >> 11);
+  thr = ldexp(1.0, 128 - (32 * (t - 2) + 43 - lz));
+}
+
+// out = |ua*A - ub*B| computed as neg ? ub*B - ua*A : ua*A - ub*B over nine
+// words; bad if that value is negative or >= 2^256 (never, for certified
+// quotients; checked all the same, the lane then takes the full-length path).
+STL_HD void lat_comb(uint32_t out[8], uint32_t ua, const uint32_t A[8], uint32_t ub, const uint32_t B[8], bool neg,
+                     bool& bad) {
+  uint64_t ca = 0, cb = 0;
+  uint32_t borrow = 0, w[9];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t pa = (uint64_t)ua * A[i] + ca, pb = (uint64_t)ub * B[i] + cb;
+    ca = pa >> 32;
+    cb = pb >> 32;
+    const uint64_t d = (uint64_t)(uint32_t)pa - (uint32_t)pb - borrow;
+    w[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  w[8] = (uint32_t)(ca - cb - borrow);
+  if (neg) {
+    uint64_t carry = 1;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const uint64_t s = (uint64_t)(~w[i]) + carry;
+      w[i] = (uint32_t)s;
+      carry = s >> 32;
+    }
+  }
+  bad = bad || w[8] != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = w[i];
+}
+
+// out = ua*A + ub*B over five words; bad on a carry out
+STL_HD void lat_madd2(uint32_t out[5], uint32_t ua, const uint32_t A[5], uint32_t ub, const uint32_t B[5], bool& bad) {
+  uint64_t ca = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint64_t pa = (uint64_t)ua * A[i] + (ca & 0xffffffffu);
+    const uint64_t s = (uint64_t)ub * B[i] + (uint32_t)pa + (ca >> 32);
+    out[i] = (uint32_t)s;
+    ca = (pa >> 32) + (s >> 32);  // < 2^33
+  }
+  bad = bad || ca != 0;
+}
+
+// One Lehmer round on the rows (larger rl, smaller rs >= 2^128 when act).
+// With M = [[m00, m01], [m10, m11]] the product of the certified steps'
+// [[q, 1], [1, 0]], (rl, rs) = M (X, Y): X = det*(m11 rl - m01 rs),
+// Y = det*(m00 rs - m10 rl), det = (-1)^steps.  Truncating to the leading
+// parts leaves |X/2^sh - x| < max(m11, m01) =: M1 and |Y/2^sh - y| < M2 :=
+// max(m10, m00), so q = floor(x / y), r = x - q y is the true quotient of
+// (X, Y) when  r >= M1 + q M2  and  y - r >= M1 + (q + 1) M2;  the step is
+// also taken only while the new remainder is certainly >= 2^128 (the exact
+// Euclid's stopping rule) and the matrix stays below 2^32.
+STL_HD void lat_lehmer_round(uint32_t rl[8], uint32_t rs[8], uint32_t tl[5], uint32_t ts[5], bool& tl_neg, bool& ok,
+                             bool act) {
+  double x, y, thr;
+  lat_lead(x, y, thr, rl, rs);
+  double m00 = 1.0, m01 = 0.0, m10 = 0.0, m11 = 1.0;
+  bool go = act, odd = false;
+#pragma unroll 1
+  for (int it = 0; it < 64; ++it) {
+    if (!lat_any(go)) break;
+    double q = floor(lat_div_est(x, y));
+    double r = fma(-q, y, x);
+    if (r < 0.0) {
+      q -= 1.0;
+      r += y;
+    } else if (r >= y) {
+      q += 1.0;
+      r -= y;
+    }
+    const double M1 = fmax(m11, m01), M2 = fmax(m10, m00);
+    const double n00 = fma(m00, q, m01), n10 = fma(m10, q, m11);
+    const double M2n = fmax(n00, n10);
+    const bool step = y > 0.0 && r >= 0.0 && r < y && r >= fma(q, M2, M1) && y - r >= fma(q + 1.0, M2, M1) &&
+                      M2n < 4294967296.0 && r - M2n >= thr;
+    go = go && step;
+    if (go) {
+      m01 = m00;
+      m00 = n00;
+      m11 = m10;
+      m10 = n10;
+      x = y;
+      y = r;
+      odd = !odd;
+    }
+  }
+  if (!act) return;
+  if (m10 != 0.0) {  // at least one certified step: apply M
+    const uint32_t u00 = (uint32_t)m00, u01 = (uint32_t)m01, u10 = (uint32_t)m10, u11 = (uint32_t)m11;
+    uint32_t X[8], Y[8], TX[5], TY[5];
+    bool bad = false;
+    lat_comb(X, u11, rl, u01, rs, odd, bad);
+    lat_comb(Y, u10, rl, u00, rs, !odd, bad);
+    lat_madd2(TX, u11, tl, u01, ts, bad);
+    lat_madd2(TY, u10, tl, u00, ts, bad);
+    bad = bad || lat_ge(Y, X);
+    ok = ok && !bad;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      rl[i] = X[i];
+      rs[i] = Y[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      tl[i] = TX[i];
+      ts[i] = TY[i];
+    }
+    tl_neg = tl_neg != odd;
+  } else {  // no certified quotient (large or near-boundary): one exact step
+    lat_step(rl, rs, tl, ts, ok);  // rl <- rl mod rs, tl <- tl + q ts
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t v = rl[i];
+      rl[i] = rs[i];
+      rs[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const uint32_t v = tl[i];
+      tl[i] = ts[i];
+      ts[i] = v;
+    }
+    tl_neg = !tl_neg;
+  }
+}
+
 // (c, d) with c == d*k (mod 8L), d odd, |c|, |d| < 2^158, as magnitudes and
 // signs.  Returns false when the lane must take the full-length path.
 STL_HD bool lattice_half(uint32_t c[5], bool& c_neg, uint32_t d[5], bool& d_neg, const uint32_t k[8]) {
-  // slot a: (ra, -ta) -- t in slot a is always <= 0; slot b: (rb, +tb) >= 0
-  uint32_t ra[8], rb[8], ta[5], tb[5];
+  // Rows (r, t) with r == t*k (mod 8L): larger (rl, tl), smaller (rs, ts),
+  // t as magnitudes; the signs alternate, tl is negative iff tl_neg.
+  uint32_t rl[8], rs[8], tl[5], ts[5];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    ra[i] = lat_N(i);
-    rb[i] = k[i];
+    rl[i] = lat_N(i);
+    rs[i] = k[i];
   }
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    ta[i] = 0;
-    tb[i] = i == 0 ? 1u : 0u;
+    tl[i] = 0;
+    ts[i] = i == 0 ? 1u : 0u;
   }
-  bool ok = true;
-  bool small_in_a = false;  // which slot holds the remainder < 2^128 at exit
-  // At most ~1.44 * 125 steps reduce a 253-bit k to 128 bits (Fibonacci worst
-  // case); 192 half-steps bound the loop for every input.
+  bool ok = true, tl_neg = true;
+  // Lehmer rounds (lat_lehmer_round): ~7 per lane for a random k, each
+  // certifying ~15 quotients from the leading 53 bits; a round that
+  // certifies none takes one exact step, so every round makes progress and
+  // 128 rounds exceed the longest Euclid sequence (~180 steps).
 #pragma unroll 1
-  for (int it = 0; it < 96; ++it) {
-    if (!ok || !lat_ge128(rb)) break;
-    lat_step(ra, rb, ta, tb, ok);  // ra < rb now
-    if (!ok || !lat_ge128(ra)) {
-      small_in_a = true;
-      break;
-    }
-    lat_step(rb, ra, tb, ta, ok);  // rb < ra now
+  for (int round = 0; round < 128; ++round) {
+    const bool act = ok && lat_ge128(rs);
+    if (!lat_any(act)) break;
+    lat_lehmer_round(rl, rs, tl, ts, tl_neg, ok, act);
   }
-  ok = ok && !(small_in_a ? lat_ge128(ra) : lat_ge128(rb));
-  // s = smaller remainder row, l = larger
-  uint32_t rs[8], rl[8], ts[5], tl[5];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    rs[i] = small_in_a ? ra[i] : rb[i];
-    rl[i] = small_in_a ? rb[i] : ra[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    ts[i] = small_in_a ? ta[i] : tb[i];
-    tl[i] = small_in_a ? tb[i] : ta[i];
-  }
-  const bool ts_neg = small_in_a, tl_neg = !small_in_a;
+  ok = ok && !lat_ge128(rs);
+  const bool ts_neg = !tl_neg;
   if (ts[0] & 1u) {
     // (c, d) = (rs, +-ts): |rs| < 2^128, |ts| <= 8L / rl < 2^128
 #pragma unroll

@@ -293,23 +293,30 @@ STL_HD bool verify_full_with_k(const uint32_t R[8], const uint32_t S[8], const u
 }
 
 // ---- half-size-scalar path (stl_lattice.h): [e]B + [c](-A) + [d](-Q) == O ----
-// Phase-1 output, 224 bytes (14 x uint4):
+// Phase-1 output, 224 bytes (14 x uint4).  Quads 0-4 (words 0-19) come from
+// the scalar half of phase 1, quads 5-13 from the point half:
 //   cdig/ddig  signed radix-16 digits 0..39 of |c|, |d| (4-bit packed)
 //   tops       bits 0-7: positions needed (max over c, d; 33 for almost
 //              every lane), bit 16 ok (pre-checks, decodings, S < L),
-//              bit 17 fallback (full-length path)
+//              bit 17 fallback (full-length path); between the two halves
+//              bit 17 = "the reduction did not fit", bits 18/19 = sign of
+//              c / d
 //   edig       signed radix-2^16 digits of e = d*S mod L (16 digits)
 //   P1, P2     affine P1 = sign(c) ? A : -A,  P2 = sign(d) ? Q : -Q
 struct HalfState {
   uint32_t cdig[5], ddig[5];
   uint32_t tops;
   uint32_t edig[8];
-  fe P1x, P1y, P2x, P2y;
   uint32_t pad;
+  fe P1x, P1y, P2x, P2y;
 };
 static_assert(sizeof(HalfState) == 224, "HalfState must be 14 x uint4");
+constexpr int kHalfScalarQuads = 5;  // quads 0-4: digits, tops, pad
+constexpr int kHalfTopsWord = 10;
 constexpr uint32_t kHalfOk = 1u << 16;
 constexpr uint32_t kHalfFallback = 1u << 17;
+constexpr uint32_t kHalfCNeg = 1u << 18;
+constexpr uint32_t kHalfDNeg = 1u << 19;
 
 // encode(P) == R is possible for some point P iff R is a canonical encoding:
 // y < p, and not "x == 0 with the sign bit set" (x == 0 <=> y == +-1).
@@ -327,8 +334,28 @@ STL_HD bool r_is_canonical(const uint32_t R[8]) {
   return !(sign && (one || pm1));
 }
 
-STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
-                               const uint32_t k[8], uint32_t policy) {
+// Phase 1, scalar half: k -> (c, d) (lattice_half) -> digits of |c|, |d|
+// and e = d*S mod L.  Light on registers and latency-bound (the Euclid
+// quotient chain, the SHA-512 rounds of k): its kernel runs at 4 waves/SIMD.
+STL_HD void verify_phase1_scalars(HalfState& o, const uint32_t S[8], const uint32_t k[8]) {
+  uint32_t c[5], d[5];
+  bool c_neg = false, d_neg = false;
+  const bool half = lattice_half(c, c_neg, d, d_neg, k);
+  uint32_t e[8];
+  sc_mul_signed(e, d, d_neg, S);
+  const int cneed = sc_recode16_half(o.cdig, c);
+  const int dneed = sc_recode16_half(o.ddig, d);
+  sc_recode65536(o.edig, e);
+  const int need = cneed > dneed ? cneed : dneed;
+  o.tops = (uint32_t)need | (half ? 0u : kHalfFallback) | (c_neg ? kHalfCNeg : 0u) | (d_neg ? kHalfDNeg : 0u);
+  o.pad = 0;
+}
+
+// Phase 1, point half: pre-checks, decompression of A and R (the two
+// pow22523 chains, register-heavy), P1 / P2 signed by the scalar half's
+// c / d signs, final ok / fallback flags in tops.
+STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
+                                 uint32_t policy) {
   bool ok = verify_prechecks(R, S, A, policy);
   // stellard composite: && signatureIsCanonical (S < L), RippleAddress.cpp:198-199
   ok = ok && sc_lt_L(S);
@@ -336,11 +363,8 @@ STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t
   bool okA, okR;
   ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
   ok = ok && okA && okR && r_is_canonical(R);
-  uint32_t c[5], d[5];
-  bool c_neg = false, d_neg = false;
-  const bool half = lattice_half(c, c_neg, d, d_neg, k);
-  uint32_t e[8];
-  sc_mul_signed(e, d, d_neg, S);
+  const bool c_neg = (o.tops & kHalfCNeg) != 0, d_neg = (o.tops & kHalfDNeg) != 0;
+  const bool fits = (o.tops & kHalfFallback) == 0;
   fe nx;
   fe_neg(nx, negA.X);
   fe_cmov(o.P1x, negA.X, nx, c_neg);
@@ -348,12 +372,13 @@ STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t
   fe_neg(nx, negQ.X);
   fe_cmov(o.P2x, negQ.X, nx, d_neg);
   o.P2y = negQ.Y;
-  const int cneed = sc_recode16_half(o.cdig, c);
-  const int dneed = sc_recode16_half(o.ddig, d);
-  sc_recode65536(o.edig, e);
-  const int need = cneed > dneed ? cneed : dneed;
-  o.tops = (uint32_t)need | (ok ? kHalfOk : 0u) | (ok && !half ? kHalfFallback : 0u);
-  o.pad = 0;
+  o.tops = (o.tops & 0xffu) | (ok ? kHalfOk : 0u) | (ok && !fits ? kHalfFallback : 0u);
+}
+
+STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
+                               const uint32_t k[8], uint32_t policy) {
+  verify_phase1_scalars(o, S, k);
+  verify_phase1_points(o, R, S, A, policy);
 }
 
 STL_HD void affine_to_p3(ge_p3& P, const fe& x, const fe& y) {

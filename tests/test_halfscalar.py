@@ -14,6 +14,7 @@ section 4) on the host build of the device code (tests/native/hostemu.cpp):
     oracle on mutated random signatures, for both policies.
 """
 import ctypes
+import math
 import random
 
 import numpy as np
@@ -77,6 +78,63 @@ def test_lattice_typical_size(emu):
         bits.append(max(abs(c).bit_length(), abs(d).bit_length()))
     # ~sqrt(8L) = 2^127.5: the doubling chain is 33 nibbles instead of 64
     assert np.median(bits) <= 128 and max(bits) <= 136
+
+
+def _to_double(x, words):
+    # lat_to_double's Horner evaluation over 32-bit words (same IEEE rounding)
+    ws = [(x >> (32 * i)) & 0xFFFFFFFF for i in range(words)]
+    d = float(ws[-1])
+    for w in reversed(ws[:-1]):
+        d = d * 4294967296.0 + float(w)
+    return d
+
+
+def _lattice_euclid(k):
+    """(ok, c, d) of the one-quotient-per-step extended Euclid on (8L, k),
+    stopped at the first remainder < 2^128, then the odd-d combination of
+    lattice_half -- the result the Lehmer reduction must reproduce exactly."""
+    rl, rs, tl, ts = N8L, k, 0, 1  # rows (r, t) with r == t*k (mod 8L), t signed
+    while rs >= 2**128:
+        q = rl // rs
+        if q >= 2**32:
+            return False, None, None
+        rl, rs, tl, ts = rs, rl - q * rs, ts, tl - q * ts
+    if ts & 1:
+        c, d = rs, ts
+    else:
+        jd = math.floor((_to_double(rl, 8) - _to_double(abs(tl), 5)) /
+                        (_to_double(rs, 8) + _to_double(abs(ts), 5)) + 0.5)
+        j = max(int(jd), 0)
+        if j >= 2**32:
+            return False, None, None
+        c = rl - j * rs
+        d = (abs(tl) + j * abs(ts)) * (1 if tl > 0 else -1)
+        if abs(c) >= 2**160 or abs(d) >= 2**160:
+            return False, None, None
+    ok = abs(c) < 2**158 and abs(d) < 2**158
+    return ok, c, d
+
+
+def _fib_ks():
+    # k/8L close to the golden ratio's convergents: all partial quotients 1,
+    # the longest quotient sequence (the Lehmer inner loop's worst case)
+    a, b, ks = 1, 1, []
+    while b < N8L:
+        a, b = b, a + b
+    ks.append(N8L * a // b)
+    ks.append(N8L * a // b + 1)
+    return [k % L for k in ks]
+
+
+def test_lattice_equals_exact_euclid(emu):
+    rng = random.Random(11)
+    ks = _boundary_ks() + _fib_ks() + [rng.randrange(L) for _ in range(20000)]
+    for k in ks:
+        ok, c, d = _lattice(emu, k)
+        rok, rc, rd = _lattice_euclid(k)
+        assert ok == rok, k
+        if ok:
+            assert (c, d) == (rc, rd), k
 
 
 def test_sc_mul_signed(emu):

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile.sh run.  Per verify kernel (pre / main /
+"""Summarise a tools/profile.sh run.  Per verify kernel (scalar / point / main /
 fallback): kernel-trace average duration, FETCH_SIZE / WRITE_SIZE per launch
 (KiB x 1024; FETCH raw and with the gfx950 x2 wide-read correction of
 MI355X_MICROARCH.md 'HBM' as an upper bound) and SQ counters; totals per
@@ -66,7 +66,7 @@ summary = {"kernels": per, "verify_launch_sequence": tot,
 json.dump(summary, open(os.path.join(d, "summary.json"), "w"), indent=1)
 if "--traffic" in sys.argv:
     json.dump({"source": f"{d}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, summed "
-                         "over verify_pre/main/fallback kernels, one verify launch sequence of the bench batch)",
+                         "over the verify_scalar/point/main/fallback kernels, one verify launch sequence of the bench batch)",
                "hbm_bytes_per_launch": tot["hbm_bytes_per_launch"],
                "hbm_bytes_per_launch_fetch_x2_upper": tot["hbm_bytes_per_launch_fetch_x2_upper"],
                "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, raw; FETCH x2 (gfx950 wide-read correction) upper bound"},
