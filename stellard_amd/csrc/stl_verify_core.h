@@ -358,11 +358,11 @@ STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32
                                  uint32_t policy) {
   bool ok = verify_prechecks(R, S, A, policy);
   // stellard composite: && signatureIsCanonical (S < L), RippleAddress.cpp:198-199
-  ok = ok && sc_lt_L(S);
+  ok = ok && sc_lt_L(S) && r_is_canonical(R);  // before the decodings: R, S not live across them
   ge_p3 negA, negQ;
   bool okA, okR;
   ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
-  ok = ok && okA && okR && r_is_canonical(R);
+  ok = ok && okA && okR;
   const bool c_neg = (o.tops & kHalfCNeg) != 0, d_neg = (o.tops & kHalfDNeg) != 0;
   const bool fits = (o.tops & kHalfFallback) == 0;
   fe nx;
