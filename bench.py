@@ -5,25 +5,38 @@ Workload (BASELINE.json configs[1]): 1,048,576 fixed-size Payment-tx
 signatures per GPU -- (R||S, 32-byte signing hash, pk) in SoA HBM buffers,
 all valid, signed on the GPU from seeded random keys/hashes before timing.
 One "step" = one stl_ed25519_verify_batch_device call over the whole batch
-(SHA-512(R||A||M), decompress, [k](-A)+[S]B, encode/compare, ballot bitmap),
-plus -- at N > 1 -- the RCCL all-gather of every rank's accept bitmap (the
-path's only exchange step).  Shards are independent per rank
-(weak scaling: every rank verifies its own 1,048,576 signatures).
+(SHA-512(R||A||M), lattice split, decompress A and R, the joint Straus check,
+ballot bitmap) plus -- at N > 1 -- libstl's RCCL gather of every rank's accept
+bitmap into rank 0 over xGMI (stl_bitmap_gather_device: the path's only
+exchange step).  Shards are independent per rank (weak scaling:
+every rank verifies its own 1,048,576 signatures, index shard
+stl_shard_range(N*n, rank, N)).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--n PER_GPU]
-  (N > 1: launched by torch.distributed.run, one process per GPU, RCCL)
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--per-gpu N_SIGS]
+
+With N > 1 and no WORLD_SIZE in the environment this process is only a
+launcher: it starts `python -m torch.distributed.run --nproc-per-node N ...
+bench.py` as a child (one process per GPU) and exits with its code -- it never
+touches the GPU itself.  Each rank: torch.distributed over gloo/TCP is the
+control plane (barriers, the RCCL unique id, max-over-ranks timing); the data
+plane is libstl (verify kernels + RCCL gather).  --dry-run rehearses the
+launcher, sharding, control plane and JSON line on CPUs only (no GPU, no
+verification; the line says so).
 
 Prints ONE JSON line on rank 0.  roofline: integer-VALU bound; achieved =
-W_VERIFY int ops per verify (frozen) x verifies per kernel launch /
-average kernel time measured with HIP events on the launch stream.
+W_VERIFY int ops per verify (frozen) x verifies per launch /
+average launch time measured with HIP events on the launch stream.
 cpu_baseline: the reference's verify call path (libsodium 1.0.18
 crypto_sign_verify_detached + stellard S<L, oracle/_ref/libsodium_ref.so) --
-or the oracle port when libsodium is absent -- on a bounded sample, rank 0 only.
+or the oracle port when libsodium is absent -- on bounded samples at T = 16
+(the GPU box's CPU share), 6 (stellard's JobQueue default) and 1 threads,
+median of 5 each, rank 0 at N = 1 only.
 """
 import argparse
-import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,6 +53,9 @@ W_VERIFY = 64 * 1520 + 36 * 1525 + 5520
 PEAK_INT_OPS = 256 * 4 * 32 * 2.4e9
 HBM_PEAK_GBS = 8000.0
 BYTES_PER_VERIFY = 64 + 32 + 32 + 1.0 / 8  # algorithmic HBM bytes (sig, msg, pk in; 1 bit out)
+# stellard's JobQueue worker count on a big host: min(ncpu, 4) + 2 (JobQueue.cpp:223-236)
+JOBQUEUE_THREADS = 6
+BOX_CPU_SHARE = 16  # CPUs a one-GPU box grants a job (OMP_NUM_THREADS there)
 
 
 def parse():
@@ -47,59 +63,140 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 19)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--per-gpu", dest="n", type=int, default=1 << 20, help="signatures per GPU")
+    ap.add_argument("--cpu-threads", type=int, default=BOX_CPU_SHARE)
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="launcher/control-plane rehearsal on CPUs, no GPU")
     return ap.parse_args()
 
 
-def cpu_baseline(sig, msg, pk, sample, threads):
-    """Host-core baseline on a bounded sample of the same workload."""
+# ------------------------------------------------------------------ launcher
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args):
+    """Start one rank per GPU as children (torch.distributed.run) and return
+    its exit code.  Nothing here imports torch or touches a device, and the
+    process is not replaced (no exec): the ranks are child processes."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------ cpu baseline
+def cpu_baseline(sig, msg, pk, threads_main, reps):
+    """Host-core baseline on bounded samples of the same workload, median of
+    `reps` runs per thread count (T = box CPU share, 6, 1)."""
     from tests import oracle_bind
-    n = min(sample, sig.shape[0])
-    s, m, p = (np.ascontiguousarray(a[:n]) for a in (sig, msg, pk))
-    threads = max(1, min(threads, os.cpu_count() or 1))
     lib = oracle_bind.load_sodium_ref()
     if lib is not None:
         kind = "reference"
-        run = lambda: oracle_bind.sodium_verify_batch(lib, s, m, p, threads=threads)  # noqa: E731
         what = (f"libsodium {lib.ref_sodium_version().decode()} crypto_sign_verify_detached + S<L "
-                "(RippleAddress::verifySignature call path)")
+                "(RippleAddress::verifySignature call path, oracle/_ref/libsodium_ref.so)")
+
+        def run(s, m, p, t):
+            return oracle_bind.sodium_verify_batch(lib, s, m, p, threads=t)
     else:
         o = oracle_bind.load_oracle()
         kind = "port"
-        run = lambda: o.verify_batch(s, m, p, threads=threads)  # noqa: E731
         what = "oracle/stl_oracle.c restatement"
-    run()  # warm
-    t0 = time.perf_counter()
-    bits = run()
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "verifies/s", "cores": threads, "kind": kind,
-            "sample": f"{n} signatures of the bench batch, {threads} threads, {what}; "
-                      f"{int(bits.sum())}/{n} accepted; {dt:.2f} s wall"}
+
+        def run(s, m, p, t):
+            return o.verify_batch(s, m, p, threads=t)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    tmain = max(1, threads_main)
+    # bounded samples: about 1 s of CPU work per run at each thread count
+    plan = [(tmain, 1 << 19), (JOBQUEUE_THREADS, 1 << 18), (1, 1 << 15)]
+    rates = {}
+    for t, cap in plan:
+        n = min(cap, sig.shape[0])
+        s, m, p = (np.ascontiguousarray(a[:n]) for a in (sig, msg, pk))
+        run(s[:256], m[:256], p[:256], t)  # warm
+        times, acc = [], None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            bits = run(s, m, p, t)
+            times.append(time.perf_counter() - t0)
+            acc = int(bits.sum())
+        med = float(np.median(times))
+        rates[str(t)] = {"verifies_per_s": n / med, "sample": n, "median_s": med, "runs": reps, "accepted": acc}
+    main_rate = rates[str(tmain)]["verifies_per_s"]
+    return {"value": main_rate, "unit": "verifies/s", "cores": tmain, "kind": kind,
+            "sample": f"first {rates[str(tmain)]['sample']} signatures of the bench batch at T={tmain} "
+                      f"(the box's CPU share; also T=6 = stellard JobQueue default and T=1 below), median of "
+                      f"{reps}; {what}",
+            "by_threads": rates, "host_nproc": os.cpu_count(), "host_affinity_cpus": avail}
 
 
-def main():
-    args = parse()
-    import torch
+# ------------------------------------------------------------------ ranks
+def control_plane(world, rank):
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    return dist
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal: launcher, shard ranges, gloo control plane, the gather
+    of bitmap words over gloo, max-over-ranks timing and the JSON line.  No
+    GPU, no verification: ``value`` counts gathered bitmap words only."""
+    import torch
+    dist = control_plane(world, rank)
     from stellard_amd import shard
+    n = args.n
+    lo, hi = shard.shard_range(n * world, rank, world)
+    words = torch.full((shard.words_per_rank(n * world, world),), -1, dtype=torch.int64)
+    for _ in range(args.warmup):
+        full = shard.gather_bitmap_words(words, n * world, world, dist) if world > 1 else words
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        full = shard.gather_bitmap_words(words, n * world, world, dist) if world > 1 else words
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t[0])
+    ok = bool(shard.words_to_bool(full, n * world).all())
+    if rank == 0:
+        print(json.dumps({
+            "metric": "DRY RUN (launcher rehearsal, no GPU, no verification)", "value": n * world * args.steps / dt,
+            "unit": "bitmap bits gathered/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u32", "data": "synthetic", "dry_run": True,
+            "config": {"workload": "dry run", "signatures_per_gpu": n, "parallelism": f"dp{world}",
+                       "rank0_shard": [lo, hi], "gathered_all_ones": ok},
+            "roofline": None, "cpu_baseline": None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def gpu_run(args, world, rank, local):
+    import torch
+    dist = control_plane(world, rank)
+    torch.cuda.set_device(local)
     from stellard_amd import verify as V
 
     V.init(device_count=1, first_device=torch.cuda.current_device())
     dev = torch.device("cuda", torch.cuda.current_device())
     n = args.n
+    lo, hi = V.shard_range(n * world, rank, world)
+    assert (lo, hi) == (rank * n, (rank + 1) * n) or n % 64, "per-rank shards are whole ballot words"
+    if world > 1:
+        # rank 0 makes the RCCL unique id; gloo carries it to every rank
+        obj = [V.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        V.comm_init_rank(world, rank, obj[0])
 
     # ---- synthetic data (outside the timed region) ----
     rng = np.random.default_rng(0x5EED0002 + rank)
@@ -107,18 +204,15 @@ def main():
     msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).to(dev)
     pk, sig = V.sign_batch_device(seeds, msgs)
     torch.cuda.synchronize()
-    words = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
-    full_words = None
+    wpr = (n + 63) // 64
+    words = torch.empty(wpr, dtype=torch.int64, device=dev)
+    full_words = torch.empty(wpr * world, dtype=torch.int64, device=dev) if world > 1 and rank == 0 else None
     stream = torch.cuda.current_stream()
-
-    def gather():
-        # rank r holds global indices [r*n, (r+1)*n): shard.shard_range(n*world, r, world)
-        return shard.gather_bitmap_words(words, n * world, world, dist)
 
     def step():
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
         if world > 1:
-            gather()
+            V.bitmap_gather_device(words, full_words, root=0, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -128,9 +222,9 @@ def main():
         raise SystemExit(f"rank {rank}: {int((~ok).sum())} valid signatures rejected -- parity failure")
 
     # ---- timed region: exactly K steps between barrier+sync on both sides ----
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -138,18 +232,18 @@ def main():
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
         ev[k][1].record(stream)
         if world > 1:
-            full_words = gather()
+            V.bitmap_gather_device(words, full_words, root=0, stream=stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt, kern_ms], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, kern_ms = float(t[0]), float(t[1])
-    if world > 1:
-        assert V.words_to_bool(full_words, n * world).all()
+    if world > 1 and rank == 0:
+        assert V.words_to_bool(full_words, n * world).all(), "gathered bitmap has rejects"
 
     if rank == 0:
         total = n * world * args.steps
@@ -168,7 +262,7 @@ def main():
                 vd = json.load(f)
             valu_busy = {"launch_pct": vd.get("launch_valu_busy_pct"),
                          "per_kernel_pct": {k: v.get("VALUBusy") for k, v in vd.get("kernels", {}).items()},
-                         "source": "rocprofv3 --pmc VALUBusy of this build, profiles/valu_latest.json"}
+                         "source": vd.get("source", "rocprofv3 --pmc VALUBusy, profiles/valu_latest.json")}
         line = {
             "metric": "Ed25519 tx verifies/sec",
             "value": value,
@@ -184,12 +278,14 @@ def main():
             "data": "synthetic: GPU-signed RFC 8032 signatures over seeded random keys and 32-byte signing hashes",
             "config": {"workload": "configs[1]: 1,048,576 fixed-size Payment-tx signatures per GPU "
                                    "(stl_ed25519_verify_batch_device, policy libsodium-1.0.18 + S<L)",
-                       "signatures_per_gpu": n, "parallelism": f"dp{world} (index shards, RCCL bitmap all-gather)"},
+                       "signatures_per_gpu": n,
+                       "parallelism": f"dp{world} (index shards, libstl RCCL bitmap gather to rank 0)"
+                                      if world > 1 else "dp1"},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
                          "kernel_ms": kern_ms, "work_per_verify": W_VERIFY,
-                         "kernels": "verify_scalar + verify_point + verify_main + verify_fallback, one stream, HIP events around "
-                                    "each stl_ed25519_verify_batch_device call",
+                         "kernels": "verify_scalar + verify_point + verify_main + verify_fallback, one stream, HIP "
+                                    "events around each stl_ed25519_verify_batch_device call",
                          "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9),
                          "valu_busy_pmc": valu_busy},
             "cpu_baseline": None,
@@ -197,12 +293,28 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(sig.cpu().numpy(), msgs.cpu().numpy(), pk.cpu().numpy(),
-                                                    args.cpu_sample, args.cpu_threads)
+                                                    args.cpu_threads, args.cpu_reps)
             except Exception as e:  # noqa: BLE001 - the baseline must not kill the GPU number
                 line["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)
     if world > 1:
+        V.comm_destroy()
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU")
+    if args.dry_run:
+        dry_run(args, world, rank)
+    else:
+        gpu_run(args, world, rank, local)
 
 
 if __name__ == "__main__":

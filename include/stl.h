@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define STL_ABI_VERSION 1
+#define STL_ABI_VERSION 2
 
 /* ---- return codes ---- */
 #define STL_OK 0
@@ -46,13 +46,17 @@ extern "C" {
 #define STL_ENODEV (-19)   /* no gfx950 device available / not initialised */
 #define STL_ENOMEM (-12)   /* device or host allocation failed */
 #define STL_EHIP (-1000)   /* HIP runtime error (kernel launch, copy, sync) */
+#define STL_ERCCL (-1001)  /* RCCL missing, communicator setup or a collective failed */
 
 /* ---- flags ---- */
 /* Accept predicate of crypto_sign_verify_detached to reproduce.  Default is
  * the container's executable oracle, libsodium 1.0.18 (S < L, R and A not of
  * small order, A canonical).  STELLARD_1_0_0 reproduces the ref10-era
  * predicate of the libsodium the reference pins (Dockerfile:9-10): only
- * (sig[63] & 0xE0) == 0; parity for it is unpinned offline. */
+ * (sig[63] & 0xE0) == 0, plus a reject of the all-zero key (as some 1.0.x
+ * releases did).  Parity for it is unpinned offline; where
+ * the offline restatement cannot be pinned the policy errs toward reject,
+ * which is the safe side -- the caller re-checks every reject serially. */
 #define STL_POLICY_SODIUM_1_0_18 0x0u
 #define STL_POLICY_STELLARD_1_0_0 0x1u
 #define STL_POLICY_MASK 0x1u
@@ -64,15 +68,28 @@ extern "C" {
  * Same accept bits, about 1.6x slower; a cross-check / reference mode. */
 #define STL_FULL_LENGTH 0x4u
 
+/* stl_config.flags.  With two or more devices the host batch calls gather the
+ * accept bitmap on device 0 with RCCL over xGMI (ncclGather / grouped
+ * send-recv into one buffer) and copy it to the host once; stl_init returns
+ * STL_ERCCL if that communicator cannot be built. */
+#define STL_CFG_RCCL_GATHER 0x1u /* use the RCCL gather even with one device */
+#define STL_CFG_NO_RCCL 0x2u     /* never use RCCL: every device copies its slice to the host */
+
 typedef struct stl_config {
-  uint32_t struct_size;  /* sizeof(stl_config) */
-  int32_t device_count;  /* devices to use; <= 0 = all visible */
-  int32_t first_device;  /* first HIP ordinal to use */
-  uint32_t flags;        /* reserved, 0 */
+  uint32_t struct_size;       /* sizeof(stl_config); the 16-byte ABI-1 struct is accepted too */
+  int32_t device_count;       /* devices to use; <= 0 = all visible */
+  int32_t first_device;       /* first HIP ordinal to use */
+  uint32_t flags;             /* STL_CFG_* */
+  int32_t shards_per_device;  /* ABI 2: host batch shards per device, each on its own host
+                                 thread (<= 0 = 1; more than 1 forces the per-device copy) */
+  uint32_t reserved;          /* 0 */
 } stl_config;
 
 /* Replaces/augments sodium_init() (src/ripple_app/ripple_app.cpp:129-132).
- * Idempotent; cfg may be NULL (all devices).  Thread-safe. */
+ * Idempotent; cfg may be NULL (all devices).  Thread-safe.  Environment
+ * overrides: STL_DEVICES (device count), STL_SHARDS_PER_DEVICE, STL_RCCL
+ * (1 = as STL_CFG_RCCL_GATHER, 0 = as STL_CFG_NO_RCCL), STL_FAULT_AFTER
+ * (stl_debug_fault_after). */
 int stl_init(const stl_config *cfg);
 void stl_shutdown(void);
 int stl_device_count(void);
@@ -82,7 +99,14 @@ const char *stl_strerror(int rc);
 /* Same signature and return convention as libsodium's
  * crypto_sign_verify_detached (0 = accept, -1 = reject), plus stellard's S<L:
  * i.e. exactly RippleAddress::verifySignature's bool as 0/-1.  Runs on the GPU
- * (batch of one); returns a value < -1 on a device error. */
+ * (batch of one); returns a value < -1 on a device error.
+ * LATENCY: one signature is one GPU lane; a call costs a few hundred
+ * microseconds (measured), several times libsodium's
+ * CPU time for a single verify, and calls serialise on the device.  Callers
+ * that verify one signature at a time (stellard's JobQueue workers) should
+ * submit through stl_batcher_* (throughput) or keep libsodium for the
+ * latency-critical single check; this entry point is the drop-in for
+ * correctness, not for speed. */
 int stl_ed25519_verify_detached(const uint8_t *sig, const uint8_t *m, unsigned long long mlen,
                                 const uint8_t *pk);
 
@@ -94,7 +118,12 @@ int stl_ed25519_verify_batch(const uint8_t *sig, const uint8_t *msg, const uint8
 
 /* checkSign equivalent: msg_i = SHA512Half(preimage_i), then verify.
  * preimage_i = preimages[offset[i] .. offset[i]+len[i]) and already includes
- * the 4-byte "STX\0" prefix (HashPrefix::txSign, HashPrefix.cpp:30). */
+ * the 4-byte "STX\0" prefix (HashPrefix::txSign, HashPrefix.cpp:30).  Any
+ * prefixed preimage works the same way, e.g. a consensus proposal's 76-byte
+ * "PRP\0" || seq || closeTime || prevLedger || position
+ * (LedgerProposal::getSigningHash, LedgerProposal.cpp:54-65).  Offsets may
+ * come in any order; with several devices the rows are split into
+ * contiguous 64-aligned shards of about equal preimage bytes. */
 int stl_tx_verify_batch(const uint8_t *preimages, const uint64_t *offset, const uint32_t *len,
                         const uint8_t *sig, const uint8_t *pk, size_t n, uint8_t *accept_bitmap,
                         uint32_t flags);
@@ -134,6 +163,22 @@ int stl_tx_hash_batch_device(const uint8_t *d_preimages, const uint64_t *d_offse
 int stl_tx_blob_verify_batch(const uint8_t *blobs, const uint64_t *offset, const uint32_t *len, size_t n,
                              uint8_t *accept_bitmap, uint8_t *status, uint8_t *tx_id, uint32_t flags);
 
+/* The same over other signed STObjects.  kind:
+ *   STL_BLOB_TRANSACTION  as stl_tx_blob_verify_batch ("STX\0", TxnSignature;
+ *                         id = SHA512Half("TXN\0" || blob))
+ *   STL_BLOB_VALIDATION   SerializedValidation::isValid(getSigningHash()):
+ *                         SHA512Half("VAL\0" || blob minus Signature) checked
+ *                         against SigningPubKey / Signature
+ *                         (SerializedValidation.cpp:70-73,96-110,
+ *                         HashPrefix.cpp:31); id = SHA512Half(blob), the
+ *                         suppression key of PeerImp::recvValidation
+ *                         (PeerImp.cpp:1148-1155); blobs shorter than 50 bytes
+ *                         (PeerImp.cpp:1134) are deferred. */
+#define STL_BLOB_TRANSACTION 0u
+#define STL_BLOB_VALIDATION 1u
+int stl_signed_blob_verify_batch(uint32_t kind, const uint8_t *blobs, const uint64_t *offset, const uint32_t *len,
+                                 size_t n, uint8_t *accept_bitmap, uint8_t *status, uint8_t *id, uint32_t flags);
+
 /* Device-resident first half: writes the verify inputs (d_msg n*32, d_sig
  * n*64, d_pk n*32; a deferred or malformed transaction gets a signature that
  * always rejects), d_status (n bytes) and, if d_tx_id is not NULL, the
@@ -142,6 +187,36 @@ int stl_tx_blob_verify_batch(const uint8_t *blobs, const uint64_t *offset, const
 int stl_tx_blob_prepare_device(const uint8_t *d_blobs, const uint64_t *d_offset, const uint32_t *d_len,
                                size_t n, uint8_t *d_msg, uint8_t *d_sig, uint8_t *d_pk, uint8_t *d_tx_id,
                                uint8_t *d_status, void *stream);
+int stl_signed_blob_prepare_device(uint32_t kind, const uint8_t *d_blobs, const uint64_t *d_offset,
+                                   const uint32_t *d_len, size_t n, uint8_t *d_msg, uint8_t *d_sig, uint8_t *d_pk,
+                                   uint8_t *d_id, uint8_t *d_status, void *stream);
+
+/* ---- multi-GPU: one process per GPU ----
+ * Verification shards by index with no exchange; the accept bitmaps are
+ * gathered with RCCL over xGMI.  rank r owns signatures
+ * [r*w*64, (r+1)*w*64) of the whole batch, w = words_per_rank (see
+ * stl_shard_range).  Setup: rank 0 calls stl_comm_unique_id and hands the
+ * 128 bytes to every rank out of band (stellard: its own config; the bench:
+ * torch.distributed over TCP); then every rank calls stl_comm_init_rank on its
+ * initialised device (blocks until all ranks have joined). */
+int stl_comm_unique_id(uint8_t id[128]);
+int stl_comm_init_rank(int nranks, int rank, const uint8_t id[128]);
+void stl_comm_destroy(void);
+/* root >= 0: ncclGather of every rank's d_words (words_per_rank u64 words)
+ * into d_all_words on rank root (nranks*words_per_rank words, rank order;
+ * other ranks may pass NULL); root < 0: ncclAllGather (every rank receives).
+ * Asynchronous on stream. */
+int stl_bitmap_gather_device(const uint64_t *d_words, size_t words_per_rank, uint64_t *d_all_words, int root,
+                             void *stream);
+
+/* Shard of [0, n) that rank r of g owns: contiguous, whole 64-signature
+ * bitmap words (the layout stl_bitmap_gather_device assumes and the host
+ * batch calls use across devices). */
+void stl_shard_range(size_t n, int r, int g, size_t *lo, size_t *hi);
+/* Byte-balanced shard for variable-length rows (config 5: preimages or blobs
+ * of 100 B - 4 KB): boundaries at the 64-aligned row where the prefix sum of
+ * len crosses r/g of the total. */
+void stl_shard_range_bytes(const uint32_t *len, size_t n, int r, int g, size_t *lo, size_t *hi);
 
 /* ---- request aggregator ----
  * stellard checks transactions one at a time on JobQueue workers
@@ -165,11 +240,25 @@ int stl_batcher_submit(stl_batcher *b, const uint8_t *sig, const uint8_t *msg32,
                        stl_verdict_fn fn, void *ctx);
 /* SerializedTransaction::checkSign for one serialized transaction (copied). */
 int stl_batcher_submit_tx(stl_batcher *b, const uint8_t *blob, size_t len, stl_verdict_fn fn, void *ctx);
-/* Returns when every request submitted before the call has completed. */
+/* Returns when every request submitted before the call has completed.
+ * Callbacks run on the aggregator's worker thread and must not call
+ * stl_batcher_flush or stl_batcher_destroy on their own aggregator. */
 void stl_batcher_flush(stl_batcher *b);
 void stl_batcher_stats(stl_batcher *b, uint64_t *submitted, uint64_t *completed, uint64_t *batches);
 /* Completes every pending request, then frees the aggregator. */
 void stl_batcher_destroy(stl_batcher *b);
+
+/* ---- testing hooks ----
+ * Fault injection: after `calls` further HIP/RCCL calls made by libstl the
+ * next one reports failure without running (one shot); calls < 0 disarms.
+ * Every entry point then returns < 0 (never a reject bitmap) and the batcher
+ * delivers the negative code as the verdict. */
+void stl_debug_fault_after(long long calls);
+/* Verify with a given k = H(R||A||M) mod L (d_k: n*32 bytes) instead of
+ * hashing: drives contrived k (the lattice reduction's full-length fallback)
+ * next to ordinary lanes in one wave. */
+int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const uint8_t *d_pk, size_t n,
+                              uint64_t *d_bitmap_words, uint32_t flags, void *stream);
 
 /* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;
  * EdKeyPair::setSeed, EdKeyPair.cpp:25-33): RFC 8032 keypair from a 32-byte

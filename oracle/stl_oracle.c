@@ -725,6 +725,11 @@ int oracle_verify_raw(const uint8_t sig[64], const uint8_t *m, size_t mlen, cons
   uint8_t h[64], k[32], rcheck[32];
   if (policy == ORACLE_POLICY_STELLARD_1_0_0) {
     if (sig[63] & 224) return -1;
+    /* the all-zero key (order 4) is rejected, as some 1.0.x releases did;
+     * unpinned offline, conservative (stl.h) */
+    int nz = 0;
+    for (int i = 0; i < 32; ++i) nz |= pk[i];
+    if (!nz) return -1;
   } else {
     if (!sc_is_canonical(sig + 32) || has_small_order(sig)) return -1;
     if (!ge_is_canonical(pk) || has_small_order(pk)) return -1;

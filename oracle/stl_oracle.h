@@ -82,11 +82,22 @@ typedef struct oracle_txinfo {
 int oracle_tx_blob(const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *full, size_t cap,
                    oracle_txinfo *info);
 
+/* The same for other signed STObjects: kind 0 = transaction (as above),
+ * kind 1 = validation ("VAL\0" prefix, signature in sfSignature, no
+ * TransactionType, at least 50 bytes: SerializedValidation.cpp:22-34,96-110,
+ * PeerImp.cpp:1134). */
+int oracle_signed_blob(uint32_t kind, const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *full, size_t cap,
+                       oracle_txinfo *info);
+
 /* checkSign over serialized transactions: bit = deserialises && |pk| = 32 &&
  * |sig| = 64 && verify(SHA512Half(signing)).  tx_id (n*32, may be NULL):
  * SHA512Half("TXN\0" || full), zero where the blob does not deserialise. */
 void oracle_tx_blob_verify_batch(const uint8_t *blobs, const uint64_t *offset, const uint32_t *len, size_t n,
                                  uint8_t *bitmap, uint8_t *tx_id, uint32_t policy, int threads);
+/* kind-generic batch; for kind 1 the id is SHA512Half(raw blob), the
+ * suppression key of PeerImp::recvValidation (PeerImp.cpp:1148-1155). */
+void oracle_signed_blob_verify_batch(uint32_t kind, const uint8_t *blobs, const uint64_t *offset, const uint32_t *len,
+                                     size_t n, uint8_t *bitmap, uint8_t *tx_id, uint32_t policy, int threads);
 
 /* Instrumentation: field multiplications / squarings executed by the last
  * single-threaded oracle_verify call (for the frozen work model). */

@@ -25,6 +25,11 @@
  *                                                 FieldNames.cpp:49-51, FieldNames.h:213-216
  *   getSigningHash / getTransactionID             SerializedObject.cpp:444-450,
  *                                                 SerializedTransaction.cpp:162-171
+ *   validations (kind 1): SerializedValidation(SerializerIterator&) and
+ *   isValid(getSigningHash()) -- "VAL\0" prefix, SigningPubKey / Signature
+ *                                                 SerializedValidation.cpp:22-34,70-73,96-110,
+ *                                                 HashPrefix.cpp:31; suppression
+ *                                                 id SHA512Half(raw), PeerImp.cpp:1134,1148-1155
  * Not restated: the transaction-type templates (TxFormats.cpp, setType);
  * duplicate top-level fields are rejected as setType would reject them.
  */
@@ -44,10 +49,12 @@ int ref_verify_signature(const unsigned char *sig, const unsigned char *hash32, 
 #define TX_SHA512(in, n, out) SHA512((in), (n), (out))
 #define TX_VERIFY(sig, h, pk, policy) (ref_verify_signature((sig), (h), (pk)) == 1) /* 1 accept */
 #define TX_BATCH_NAME ref_tx_blob_verify_batch
+#define KIND_BATCH_NAME ref_signed_blob_verify_batch
 #else
 #define TX_SHA512(in, n, out) oracle_sha512((in), (n), (out))
 #define TX_VERIFY(sig, h, pk, policy) (oracle_verify((sig), (h), 32, (pk), (policy)) == 0)
 #define TX_BATCH_NAME oracle_tx_blob_verify_batch
+#define KIND_BATCH_NAME oracle_signed_blob_verify_batch
 #endif
 
 /* ---------------------------------------------------------------- buffers */
@@ -463,26 +470,29 @@ static long vl_payload(const flist_t *l, uint32_t code, uint8_t *dst, size_t cap
   return -1;
 }
 
-int oracle_tx_blob(const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *full, size_t cap,
-                   oracle_txinfo *info) {
+int oracle_signed_blob(uint32_t kind, const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *full,
+                       size_t cap, oracle_txinfo *info) {
   memset(info, 0, sizeof *info);
   info->pk_len = info->sig_len = -1;
-  /* SerializedTransaction.cpp:68-74 */
-  if (len < 32 || len > 1024 * 1024) return -1;
+  if (kind > 1) return -1;
+  /* transactions: SerializedTransaction.cpp:68-74; validations: PeerImp.cpp:1134 */
+  if (len < (kind == 0 ? 32u : 50u) || len > 1024 * 1024) return -1;
   rd_t r = {blob, len, 0, 0, 1, 0};
   flist_t top = {0};
   info->stopped_early = parse_object(&r, 0, &top) && r.pos < len ? 1 : 0;
   int rc = 0;
   if (r.err || has_duplicates(&top)) rc = -1;
-  int has_type = 0;
-  for (size_t i = 0; i < top.n; ++i) has_type |= top.f[i].code == 0x10002u; /* getFieldU16(sfTransactionType) */
-  if (!has_type) rc = -1;
+  if (kind == 0) {
+    int has_type = 0;
+    for (size_t i = 0; i < top.n; ++i) has_type |= top.f[i].code == 0x10002u; /* getFieldU16(sfTransactionType) */
+    if (!has_type) rc = -1;
+  }
   info->all_declared = r.all_declared;
   info->max_depth = r.max_depth;
   if (rc == 0) {
     buf_t s = {0}, f = {0};
-    const uint8_t pfx[4] = {'S', 'T', 'X', 0};
-    buf_put(&s, pfx, 4);
+    const uint8_t pfx_tx[4] = {'S', 'T', 'X', 0}, pfx_val[4] = {'V', 'A', 'L', 0};
+    buf_put(&s, kind == 0 ? pfx_tx : pfx_val, 4);
     add_sorted(&top, &s, 0);
     add_sorted(&top, &f, 1);
     if (s.n > cap || f.n > cap) {
@@ -496,10 +506,16 @@ int oracle_tx_blob(const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *f
     free(s.p);
     free(f.p);
     info->pk_len = vl_payload(&top, 0x70003u, info->pk, sizeof info->pk);
-    info->sig_len = vl_payload(&top, 0x70004u, info->sig, sizeof info->sig);
+    /* TxnSignature (checkSign) or Signature (SerializedValidation::isValid) */
+    info->sig_len = vl_payload(&top, kind == 0 ? 0x70004u : 0x70006u, info->sig, sizeof info->sig);
   }
   flist_free(&top);
   return rc;
+}
+
+int oracle_tx_blob(const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *full, size_t cap,
+                   oracle_txinfo *info) {
+  return oracle_signed_blob(0, blob, len, signing, full, cap, info);
 }
 
 /* ---------------------------------------------------------------- batch */
@@ -511,6 +527,7 @@ typedef struct {
   uint8_t *bits; /* one byte per tx */
   uint8_t *tx_id;
   uint32_t policy;
+  uint32_t kind;
 } blob_job_t;
 
 static void *blob_worker(void *arg) {
@@ -527,18 +544,21 @@ static void *blob_worker(void *arg) {
     oracle_txinfo info;
     uint8_t ok = 0;
     uint8_t h[64];
-    if (oracle_tx_blob(j->blobs + j->off[i], n, s, f, cap, &info) == 0) {
+    if (oracle_signed_blob(j->kind, j->blobs + j->off[i], n, s, f, cap, &info) == 0) {
       if (info.pk_len == 32 && info.sig_len == 64) {
         TX_SHA512(s, info.signing_len, h);
         ok = TX_VERIFY(info.sig, h, info.pk, j->policy) ? 1 : 0;
       }
-      if (j->tx_id) {
+      if (j->tx_id && j->kind == 0) {
         uint8_t *t = (uint8_t *)malloc(info.full_len + 4);
         t[0] = 'T'; t[1] = 'X'; t[2] = 'N'; t[3] = 0;
         memcpy(t + 4, f, info.full_len);
         TX_SHA512(t, info.full_len + 4, h);
         memcpy(j->tx_id + 32 * i, h, 32);
         free(t);
+      } else if (j->tx_id) { /* validation suppression id: the raw bytes */
+        TX_SHA512(j->blobs + j->off[i], n, h);
+        memcpy(j->tx_id + 32 * i, h, 32);
       }
     } else if (j->tx_id) {
       memset(j->tx_id + 32 * i, 0, 32);
@@ -550,8 +570,16 @@ static void *blob_worker(void *arg) {
   return NULL;
 }
 
+void KIND_BATCH_NAME(uint32_t kind, const uint8_t *blobs, const uint64_t *offset, const uint32_t *len, size_t n,
+                     uint8_t *bitmap, uint8_t *tx_id, uint32_t policy, int threads);
+
 void TX_BATCH_NAME(const uint8_t *blobs, const uint64_t *offset, const uint32_t *len, size_t n,
                                  uint8_t *bitmap, uint8_t *tx_id, uint32_t policy, int threads) {
+  KIND_BATCH_NAME(0, blobs, offset, len, n, bitmap, tx_id, policy, threads);
+}
+
+void KIND_BATCH_NAME(uint32_t kind, const uint8_t *blobs, const uint64_t *offset, const uint32_t *len, size_t n,
+                     uint8_t *bitmap, uint8_t *tx_id, uint32_t policy, int threads) {
   if (threads < 1) threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
   if (threads < 1) threads = 1;
   uint8_t *bits = (uint8_t *)calloc(n ? n : 1, 1);
@@ -567,6 +595,7 @@ void TX_BATCH_NAME(const uint8_t *blobs, const uint64_t *offset, const uint32_t 
     jobs[t].bits = bits;
     jobs[t].tx_id = tx_id;
     jobs[t].policy = policy;
+    jobs[t].kind = kind;
     pthread_create(&th[t], NULL, blob_worker, &jobs[t]);
   }
   for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);

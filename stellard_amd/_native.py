@@ -15,6 +15,15 @@ STL_EINVAL = -22
 STL_ENODEV = -19
 STL_ENOMEM = -12
 STL_EHIP = -1000
+STL_ERCCL = -1001
+
+# stl_config.flags
+STL_CFG_RCCL_GATHER = 0x1
+STL_CFG_NO_RCCL = 0x2
+
+# signed-object kinds of the blob entry points
+STL_BLOB_TRANSACTION = 0
+STL_BLOB_VALIDATION = 1
 
 STL_POLICY_SODIUM_1_0_18 = 0x0
 STL_POLICY_STELLARD_1_0_0 = 0x1
@@ -54,6 +63,18 @@ SYMBOLS = [
     ("stl_batcher_flush", None, [_P]),
     ("stl_batcher_stats", None, [_P, _P, _P, _P]),
     ("stl_batcher_destroy", None, [_P]),
+    ("stl_signed_blob_verify_batch", ctypes.c_int,
+     [ctypes.c_uint32, _U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, ctypes.c_uint32]),
+    ("stl_signed_blob_prepare_device", ctypes.c_int,
+     [ctypes.c_uint32, _U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, _U8P, _U8P, _P]),
+    ("stl_comm_unique_id", ctypes.c_int, [_U8P]),
+    ("stl_comm_init_rank", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _U8P]),
+    ("stl_comm_destroy", None, []),
+    ("stl_bitmap_gather_device", ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_int, _P]),
+    ("stl_shard_range", None, [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _P, _P]),
+    ("stl_shard_range_bytes", None, [_P, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _P, _P]),
+    ("stl_debug_fault_after", None, [ctypes.c_longlong]),
+    ("stl_debug_verify_k_device", ctypes.c_int, [_U8P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
 ]
 
 VERDICT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)

@@ -1,15 +1,29 @@
 // stl_api.cpp -- host side of libstl: the extern "C" boundary declared in
-// include/stl.h.  Owns devices, streams, workspaces and staging buffers; has
-// no CPU verification path (a device failure returns < 0 and the caller --
-// stellard -- falls back to libsodium, as SURVEY.md section 8b requires).
+// include/stl.h.  Owns devices, streams, workspaces, staging buffers and RCCL
+// communicators; has no CPU verification path (a device failure returns < 0
+// and the caller -- stellard -- falls back to libsodium, as SURVEY.md
+// section 8b requires).
 //
 // Threading: stellard calls verify concurrently from JobQueue workers
 // (JobQueue.cpp:217-243).  Every device has a mutex that serialises the host
-// batch entry points on that device; the device-resident entry points key
-// their workspace by (device, stream) so concurrent streams never share one.
+// batch entry points on that device; a batch that gathers over RCCL holds
+// every device's mutex for its whole run.  The device-resident entry points
+// key their workspace by (device, stream) so concurrent streams never share
+// one.
+//
+// Multi-GPU: a host batch is split into contiguous 64-aligned
+// shards (by index, or by preimage bytes for variable-length rows), one host
+// thread per shard.  With two or more devices each device keeps its slice of
+// the accept bitmap in HBM and RCCL gathers the slices into device 0 over
+// xGMI (ncclGather for equal slices, grouped send/recv for byte-balanced
+// ones), then one copy brings the bitmap to the host.  One process per GPU
+// uses stl_comm_* + stl_bitmap_gather_device instead.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -23,11 +37,74 @@
 
 namespace {
 
+// ---- fault injection (stl_debug_fault_after) --------------------------------
+// A countdown over the HIP / RCCL calls libstl checks; the call at which it
+// reaches zero is not executed and reports failure.  One shot.
+std::atomic<long long> g_fault_after{-1};
+
+bool fault_now() {
+  long long v = g_fault_after.load(std::memory_order_relaxed);
+  while (v >= 0) {
+    if (g_fault_after.compare_exchange_weak(v, v - 1, std::memory_order_relaxed)) return v == 0;
+  }
+  return false;
+}
+
 #define STL_TRY(expr)                        \
   do {                                       \
+    if (fault_now()) return STL_EHIP;        \
     hipError_t e_ = (expr);                  \
     if (e_ != hipSuccess) return STL_EHIP;   \
   } while (0)
+
+#define STL_RCCL_TRY(expr)                   \
+  do {                                       \
+    if (fault_now()) return STL_ERCCL;       \
+    ncclResult_t r_ = (expr);                \
+    if (r_ != ncclSuccess) return STL_ERCCL; \
+  } while (0)
+
+#define STL_RC(expr)        \
+  do {                      \
+    int rc_ = (expr);       \
+    if (rc_) return rc_;    \
+  } while (0)
+
+// ---- RCCL, loaded on first use (libstl does not need it on one device) ----
+struct Rccl {
+  std::once_flag once;
+  bool ok = false;
+  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclGather) Gather = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclSend) Send = nullptr;
+  decltype(&ncclRecv) Recv = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+
+  template <typename F>
+  static bool sym(void* h, const char* name, F& f) {
+    f = reinterpret_cast<F>(dlsym(h, name));
+    return f != nullptr;
+  }
+  bool load() {
+    std::call_once(once, [this] {
+      // an already loaded librccl (e.g. PyTorch's) is reused by soname
+      void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) return;
+      ok = sym(h, "ncclGetUniqueId", GetUniqueId) && sym(h, "ncclCommInitRank", CommInitRank) &&
+           sym(h, "ncclCommInitAll", CommInitAll) && sym(h, "ncclCommDestroy", CommDestroy) &&
+           sym(h, "ncclGather", Gather) && sym(h, "ncclAllGather", AllGather) && sym(h, "ncclSend", Send) &&
+           sym(h, "ncclRecv", Recv) && sym(h, "ncclGroupStart", GroupStart) && sym(h, "ncclGroupEnd", GroupEnd);
+    });
+    return ok;
+  }
+};
+Rccl g_rccl;
 
 struct DevBuf {
   void* p = nullptr;
@@ -37,7 +114,10 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    if (hipMalloc(&p, bytes) != hipSuccess) return STL_ENOMEM;
+    if (fault_now() || hipMalloc(&p, bytes) != hipSuccess) {
+      p = nullptr;
+      return STL_ENOMEM;
+    }
     cap = bytes;
     return STL_OK;
   }
@@ -54,8 +134,9 @@ struct Device {
   uint32_t grid = 0;  // resident workgroups for the verify kernel
   hipStream_t stream = nullptr;  // kernels of the host batch API
   hipStream_t copy = nullptr;    // its host-to-device copies (overlap the previous chunk's kernels)
+  ncclComm_t comm = nullptr;     // in-process communicator (rank = device index)
   std::mutex mu;
-  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide;
+  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide, gather;
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;  // tx-hash work counter
   std::mutex ws_mu;
@@ -64,6 +145,13 @@ struct Device {
 std::mutex g_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
 bool g_init = false;
+int g_shards_per_device = 1;
+bool g_comm_gather = false;  // host batches gather their bitmap over RCCL
+
+// one process per GPU (stl_comm_*)
+std::mutex g_pcomm_mu;
+ncclComm_t g_pcomm = nullptr;
+int g_pcomm_ranks = 0;
 
 int current_device_index() {
   int ord = -1;
@@ -86,15 +174,33 @@ int setup_device(Device& d) {
   STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   STL_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
   // wide base tables for [e]B (7.3 MB), built once on the device
-  int rc = d.wide.ensure(stl::kWideTableBytes);
-  if (rc) return rc;
+  STL_RC(d.wide.ensure(stl::kWideTableBytes));
   STL_TRY(stl::launch_wide_table(static_cast<uint4*>(d.wide.p), d.stream));
   STL_TRY(hipStreamSynchronize(d.stream));
   return STL_OK;
 }
 
+void release_device(Device& d) {
+  (void)hipSetDevice(d.ordinal);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.copy) (void)hipStreamSynchronize(d.copy);
+  if (d.comm && g_rccl.ok) (void)g_rccl.CommDestroy(d.comm);
+  d.comm = nullptr;
+  for (DevBuf* b : {&d.ws, &d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.txid, &d.status,
+                    &d.wide, &d.gather})
+    b->release();
+  for (auto& kv : d.stream_ws) kv.second->release();
+  for (auto& kv : d.stream_ctr) kv.second->release();
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  if (d.copy) (void)hipStreamDestroy(d.copy);
+  d.stream = d.copy = nullptr;
+}
+
 int ensure_init() {
-  if (g_init) return STL_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_init) return STL_OK;
+  }
   return stl_init(nullptr);
 }
 
@@ -103,8 +209,7 @@ int stream_workspace(Device& d, hipStream_t s, uint4** ws) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
   auto& slot = d.stream_ws[s];
   if (!slot) slot.reset(new DevBuf());
-  int rc = slot->ensure(stl::verify_ws_bytes(d.grid));
-  if (rc) return rc;
+  STL_RC(slot->ensure(stl::verify_ws_bytes(d.grid)));
   *ws = static_cast<uint4*>(slot->p);
   return STL_OK;
 }
@@ -115,8 +220,7 @@ int stream_queue(Device& d, hipStream_t s, size_t n, uint32_t** qws) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
   auto& slot = d.stream_ctr[s];
   if (!slot) slot.reset(new DevBuf());
-  int rc = slot->ensure(stl::hash_queue_bytes(n));
-  if (rc) return rc;
+  STL_RC(slot->ensure(stl::hash_queue_bytes(n)));
   *qws = static_cast<uint32_t*>(slot->p);
   return STL_OK;
 }
@@ -129,7 +233,7 @@ uint32_t grid_for(const Device& d, size_t n) {
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(tiles, d.grid));
 }
 
-// Contiguous 64-aligned shard of [0, n) for device r of g.
+// Contiguous 64-aligned shard of [0, n) for shard r of g (stl_shard_range).
 void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
   const size_t words = (n + 63) / 64;
   const size_t per = (words + g - 1) / g;
@@ -137,23 +241,54 @@ void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
   *hi = std::min(n, (size_t)(r + 1) * per * 64);
 }
 
-// ---- host batch API: chunked copy/compute pipeline ----
+// Byte-balanced 64-aligned shard boundaries: bound[r] = the 64-aligned row at
+// or after the first row whose byte prefix sum reaches r/g of the total.
+void shard_bytes_bounds(const uint32_t* len, size_t n, int g, std::vector<size_t>& bound) {
+  bound.assign(g + 1, n);
+  bound[0] = 0;
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += len[i];
+  uint64_t acc = 0;
+  size_t i = 0;
+  for (int r = 1; r < g; ++r) {
+    const uint64_t target = (uint64_t)((__uint128_t)total * (unsigned)r / (unsigned)g);
+    while (i < n && acc < target) acc += len[i++];
+    const size_t b = std::min(n, (i + 63) / 64 * 64);
+    bound[r] = std::max(bound[r - 1], b);
+  }
+}
+
+// ---- host batch API ---------------------------------------------------------
 // A shard is processed in chunks of kPipeChunk signatures (a multiple of 64,
 // so every chunk starts on a bitmap word).  Chunk c's inputs are copied on
 // d.copy while chunk c-1's kernels run on d.stream; an event orders each
 // chunk's kernels after its copy.  Device buffers hold the whole shard, so no
 // buffer is reused while a kernel may still read it.  Variable-length bytes
 // (preimages, blobs) are copied up to a watermark: chunk c copies
-// [watermark, max end of its rows), which is the whole contiguous range when
-// offsets ascend and stays correct for any order (rows below the watermark
-// were copied by an earlier chunk).
+// [watermark, max end of its rows), rebased on the shard's lowest offset, so
+// any offset order is correct.
 constexpr size_t kPipeChunk = (size_t)1 << 18;
 
-struct Pipeline {
-  Device& d;
+enum class Mode { kSig, kPre, kBlob };
+
+struct Batch {
+  Mode mode;
+  const uint8_t *sig, *msg32, *pk, *bytes;  // bytes: preimages or blobs
+  const uint64_t* off;
+  const uint32_t* len;
+  uint8_t *bitmap, *status, *txid;
+  uint32_t policy, kind;
+};
+
+// Host-side state of one shard; lives until the batch has synchronised (the
+// staging vectors are sources of asynchronous copies).
+struct Shard {
+  Device* d = nullptr;
+  size_t lo = 0, hi = 0;
+  std::vector<uint64_t> roff, row_end;
   std::vector<hipEvent_t> ev;
-  explicit Pipeline(Device& dev) : d(dev) {}
-  ~Pipeline() {
+  int rc = STL_OK;
+  ~Shard() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   }
   // Make d.stream wait for everything issued on d.copy so far.
@@ -161,172 +296,236 @@ struct Pipeline {
     hipEvent_t e;
     STL_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ev.push_back(e);
-    STL_TRY(hipEventRecord(e, d.copy));
-    STL_TRY(hipStreamWaitEvent(d.stream, e, 0));
+    STL_TRY(hipEventRecord(e, d->copy));
+    STL_TRY(hipStreamWaitEvent(d->stream, e, 0));
     return STL_OK;
   }
 };
 
 // Rebased offsets of rows [lo, hi) and the byte range they span.
-int rebase(const uint64_t* off, const uint32_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff,
-           std::vector<uint64_t>& row_end, uint64_t* base_out, uint64_t* bytes_out) {
+void rebase(const uint64_t* off, const uint32_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff,
+            std::vector<uint64_t>& row_end, uint64_t* base_out, uint64_t* bytes_out) {
   const size_t n = hi - lo;
-  const uint64_t base = off[lo];
-  uint64_t end = base;
+  uint64_t base = off[lo], end = 0;
+  for (size_t i = lo; i < hi; ++i) base = std::min(base, off[i]);
   roff.resize(n);
   row_end.resize(n);
   for (size_t i = 0; i < n; ++i) {
-    if (off[lo + i] < base) return STL_EINVAL;
     roff[i] = off[lo + i] - base;
     row_end[i] = roff[i] + len[lo + i];
-    end = std::max<uint64_t>(end, off[lo + i] + len[lo + i]);
+    end = std::max(end, row_end[i]);
   }
   *base_out = base;
-  *bytes_out = end - base;
-  return STL_OK;
+  *bytes_out = end;
 }
 
 // Copy the bytes rows [c0, c1) need that are not on the device yet.
-int copy_rows(Pipeline& pl, uint8_t* dst, const uint8_t* src, const std::vector<uint64_t>& row_end, size_t c0,
-              size_t c1, uint64_t* watermark) {
+int copy_rows(Shard& s, uint8_t* dst, const uint8_t* src, size_t c0, size_t c1, uint64_t* watermark) {
   uint64_t need = *watermark;
-  for (size_t i = c0; i < c1; ++i) need = std::max(need, row_end[i]);
+  for (size_t i = c0; i < c1; ++i) need = std::max(need, s.row_end[i]);
   if (need > *watermark)
-    STL_TRY(hipMemcpyAsync(dst + *watermark, src + *watermark, need - *watermark, hipMemcpyHostToDevice, pl.d.copy));
+    STL_TRY(hipMemcpyAsync(dst + *watermark, src + *watermark, need - *watermark, hipMemcpyHostToDevice, s.d->copy));
   *watermark = need;
   return STL_OK;
 }
 
-// Verify one shard [lo, hi) on device d, synchronously; writes the host bitmap
-// bytes [lo/8, ceil(hi/8)).  msg32 == nullptr means tx mode (preimages).
-int run_shard(Device& d, const uint8_t* sig, const uint8_t* msg32, const uint8_t* pk, const uint8_t* pre,
-              const uint64_t* off, const uint32_t* len, size_t lo, size_t hi, uint8_t* bitmap, uint32_t policy) {
-  const size_t n = hi - lo;
-  if (n == 0) return STL_OK;
-  std::lock_guard<std::mutex> lk(d.mu);
+// Enqueue shard [lo, hi) of the batch on its device: copies, kernels, and the
+// device-to-host copies of status / ids.  The accept bitmap stays in
+// d.bitmap (words [0, ceil(n/64))).  Caller holds d.mu and synchronises.
+int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
+  Device& d = *s.d;
+  const size_t lo = s.lo, n = s.hi - s.lo;
   STL_TRY(hipSetDevice(d.ordinal));
-  int rc;
-  const size_t words = (n + 63) / 64;
-  if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(n * 64)) ||
-      (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)))
-    return rc;
-  std::vector<uint64_t> roff, row_end;
+  STL_RC(d.bitmap.ensure(std::max<size_t>(words_alloc, 1) * 8));
+  if (n == 0) return STL_OK;
+  STL_RC(d.ws.ensure(stl::verify_ws_bytes(d.grid)));
+  STL_RC(d.sig.ensure(n * 64));
+  STL_RC(d.msg.ensure(n * 32));
+  STL_RC(d.pk.ensure(n * 32));
   uint64_t base = 0, bytes = 0, mark = 0;
-  if (!msg32) {
-    if ((rc = rebase(off, len, lo, hi, roff, row_end, &base, &bytes))) return rc;
-    if ((rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
-        (rc = d.ctr.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk)))))
-      return rc;
-    STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, d.copy));
-    STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, d.copy));
-  }
-  Pipeline pl(d);
   uint8_t* dsig = static_cast<uint8_t*>(d.sig.p);
   uint8_t* dmsg = static_cast<uint8_t*>(d.msg.p);
   uint8_t* dpk = static_cast<uint8_t*>(d.pk.p);
-  for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
-    const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
-    STL_TRY(hipMemcpyAsync(dsig + 64 * c0, sig + 64 * (lo + c0), cn * 64, hipMemcpyHostToDevice, d.copy));
-    STL_TRY(hipMemcpyAsync(dpk + 32 * c0, pk + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
-    if (msg32) {
-      STL_TRY(hipMemcpyAsync(dmsg + 32 * c0, msg32 + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
-    } else if ((rc = copy_rows(pl, static_cast<uint8_t*>(d.pre.p), pre + base, row_end, c0, c1, &mark))) {
-      return rc;
+  uint8_t* dpre = nullptr;
+  uint64_t* doff = nullptr;
+  uint32_t* dlen = nullptr;
+  if (b.mode != Mode::kSig) {
+    rebase(b.off, b.len, lo, s.hi, s.roff, s.row_end, &base, &bytes);
+    STL_RC(d.pre.ensure(bytes + 16));
+    STL_RC(d.off.ensure(n * 8));
+    STL_RC(d.len.ensure(n * 4));
+    STL_RC(d.ctr.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
+    if (b.mode == Mode::kBlob) {
+      STL_RC(d.status.ensure(n));
+      if (b.txid) STL_RC(d.txid.ensure(n * 32));
     }
-    if ((rc = pl.join_copy())) return rc;
-    if (!msg32)
-      STL_TRY(stl::launch_tx_hash(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p) + c0,
-                                  static_cast<uint32_t*>(d.len.p) + c0, (uint32_t)cn, dmsg + 32 * c0,
-                                  static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream));
-    STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
-                               static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, policy, static_cast<uint4*>(d.ws.p),
-                               grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream));
+    dpre = static_cast<uint8_t*>(d.pre.p);
+    doff = static_cast<uint64_t*>(d.off.p);
+    dlen = static_cast<uint32_t*>(d.len.p);
+    STL_TRY(hipMemcpyAsync(doff, s.roff.data(), n * 8, hipMemcpyHostToDevice, d.copy));
+    STL_TRY(hipMemcpyAsync(dlen, b.len + lo, n * 4, hipMemcpyHostToDevice, d.copy));
   }
-  std::vector<uint8_t> host_words(words * 8);
-  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, d.stream));
-  STL_TRY(hipStreamSynchronize(d.stream));
-  // lo is a multiple of 64, so the shard starts on a byte boundary
-  std::memcpy(bitmap + lo / 8, host_words.data(), (n + 7) / 8);
-  return STL_OK;
-}
-
-// Serialized-transaction shard [lo, hi) on device d: canonical pass, hashes,
-// verify; writes the host bitmap bytes and, when asked, status and tx ids.
-int run_blob_shard(Device& d, const uint8_t* blobs, const uint64_t* off, const uint32_t* len, size_t lo, size_t hi,
-                   uint8_t* bitmap, uint8_t* status, uint8_t* txid, uint32_t policy) {
-  const size_t n = hi - lo;
-  if (n == 0) return STL_OK;
-  std::lock_guard<std::mutex> lk(d.mu);
-  STL_TRY(hipSetDevice(d.ordinal));
-  int rc;
-  const size_t words = (n + 63) / 64;
-  std::vector<uint64_t> roff, row_end;
-  uint64_t base = 0, bytes = 0, mark = 0;
-  if ((rc = rebase(off, len, lo, hi, roff, row_end, &base, &bytes))) return rc;
-  if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(n * 64)) ||
-      (rc = d.msg.ensure(n * 32)) || (rc = d.pk.ensure(n * 32)) || (rc = d.bitmap.ensure(words * 8)) ||
-      (rc = d.pre.ensure(bytes + 4)) || (rc = d.off.ensure(n * 8)) || (rc = d.len.ensure(n * 4)) ||
-      (rc = d.ctr.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk)))) || (rc = d.status.ensure(n)) ||
-      (txid && (rc = d.txid.ensure(n * 32))))
-    return rc;
-  Pipeline pl(d);
-  STL_TRY(hipMemcpyAsync(d.off.p, roff.data(), n * 8, hipMemcpyHostToDevice, d.copy));
-  STL_TRY(hipMemcpyAsync(d.len.p, len + lo, n * 4, hipMemcpyHostToDevice, d.copy));
-  uint8_t* dsig = static_cast<uint8_t*>(d.sig.p);
-  uint8_t* dmsg = static_cast<uint8_t*>(d.msg.p);
-  uint8_t* dpk = static_cast<uint8_t*>(d.pk.p);
-  uint8_t* dtxid = txid ? static_cast<uint8_t*>(d.txid.p) : nullptr;
+  uint8_t* dtxid = (b.mode == Mode::kBlob && b.txid) ? static_cast<uint8_t*>(d.txid.p) : nullptr;
+  uint8_t* dstatus = b.mode == Mode::kBlob ? static_cast<uint8_t*>(d.status.p) : nullptr;
   for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
     const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
-    if ((rc = copy_rows(pl, static_cast<uint8_t*>(d.pre.p), blobs + base, row_end, c0, c1, &mark))) return rc;
-    if ((rc = pl.join_copy())) return rc;
-    STL_TRY(stl::launch_tx_blob(static_cast<uint8_t*>(d.pre.p), static_cast<uint64_t*>(d.off.p) + c0,
-                                static_cast<uint32_t*>(d.len.p) + c0, (uint32_t)cn, dmsg + 32 * c0, dsig + 64 * c0,
-                                dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr,
-                                static_cast<uint8_t*>(d.status.p) + c0, static_cast<uint32_t*>(d.ctr.p),
-                                hash_grid(d), d.stream));
+    if (b.mode != Mode::kBlob) {
+      STL_TRY(hipMemcpyAsync(dsig + 64 * c0, b.sig + 64 * (lo + c0), cn * 64, hipMemcpyHostToDevice, d.copy));
+      STL_TRY(hipMemcpyAsync(dpk + 32 * c0, b.pk + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
+    }
+    if (b.mode == Mode::kSig)
+      STL_TRY(hipMemcpyAsync(dmsg + 32 * c0, b.msg32 + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
+    else
+      STL_RC(copy_rows(s, dpre, b.bytes + base, c0, c1, &mark));
+    STL_RC(s.join_copy());
+    if (b.mode == Mode::kPre)
+      STL_TRY(stl::launch_tx_hash(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0,
+                                  static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream));
+    else if (b.mode == Mode::kBlob)
+      STL_TRY(stl::launch_tx_blob(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, dsig + 64 * c0,
+                                  dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0,
+                                  static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream, b.kind));
     STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
-                               static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, policy, static_cast<uint4*>(d.ws.p),
+                               static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, static_cast<uint4*>(d.ws.p),
                                grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream));
   }
-  std::vector<uint8_t> host_words(words * 8);
-  STL_TRY(hipMemcpyAsync(host_words.data(), d.bitmap.p, words * 8, hipMemcpyDeviceToHost, d.stream));
-  if (status) STL_TRY(hipMemcpyAsync(status + lo, d.status.p, n, hipMemcpyDeviceToHost, d.stream));
-  if (txid) STL_TRY(hipMemcpyAsync(txid + 32 * lo, d.txid.p, n * 32, hipMemcpyDeviceToHost, d.stream));
-  STL_TRY(hipStreamSynchronize(d.stream));
-  std::memcpy(bitmap + lo / 8, host_words.data(), (n + 7) / 8);
+  if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
+  if (dtxid) STL_TRY(hipMemcpyAsync(b.txid + 32 * lo, dtxid, n * 32, hipMemcpyDeviceToHost, d.stream));
   return STL_OK;
 }
 
-int run_batch(const uint8_t* sig, const uint8_t* msg32, const uint8_t* pk, const uint8_t* pre, const uint64_t* off,
-              const uint32_t* len, size_t n, uint8_t* bitmap, uint32_t flags) {
+// Wait for everything a shard enqueued, whatever happened (an error return
+// must not leave copies that read or write the caller's buffers in flight).
+int drain(Device& d) {
+  (void)hipSetDevice(d.ordinal);
+  const hipError_t a = hipStreamSynchronize(d.copy);
+  const hipError_t b = hipStreamSynchronize(d.stream);
+  return (a == hipSuccess && b == hipSuccess) ? STL_OK : STL_EHIP;
+}
+
+// Per-device copy: the shard's bitmap words to the host bitmap bytes
+// [lo/8, ceil(hi/8)).  lo is a multiple of 64, so the slice is byte aligned.
+int finish_direct(const Batch& b, Shard& s, std::vector<uint8_t>& host_words) {
+  const size_t n = s.hi - s.lo;
   if (n == 0) return STL_OK;
-  if (!sig || !pk || !bitmap || (!msg32 && (!pre || !off || !len))) return STL_EINVAL;
-  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) return STL_EINVAL;
-  int rc = ensure_init();
+  host_words.resize((n + 63) / 64 * 8);
+  STL_TRY(hipMemcpyAsync(host_words.data(), s.d->bitmap.p, host_words.size(), hipMemcpyDeviceToHost, s.d->stream));
+  STL_TRY(hipStreamSynchronize(s.d->stream));
+  std::memcpy(b.bitmap + s.lo / 8, host_words.data(), (n + 7) / 8);
+  return STL_OK;
+}
+
+int run_shard_direct(const Batch& b, Shard& s) {
+  std::lock_guard<std::mutex> lk(s.d->mu);
+  int rc = enqueue_shard(b, s, (s.hi - s.lo + 63) / 64);
+  std::vector<uint8_t> host_words;
+  if (rc == STL_OK) rc = finish_direct(b, s, host_words);
+  const int drc = drain(*s.d);
+  return rc ? rc : drc;
+}
+
+// RCCL gather of every shard's words into device 0, then one copy to the host.
+// Shards are one per device in device order; `equal` = index shards (every
+// shard `per` words, ncclGather), else grouped send/recv at each shard's word
+// offset.
+int gather_to_host(const Batch& b, std::vector<Shard>& sh, size_t n, size_t per, bool equal) {
+  const int g = (int)sh.size();
+  Device& root = *sh[0].d;
+  const size_t words = (n + 63) / 64;
+  STL_TRY(hipSetDevice(root.ordinal));
+  STL_RC(root.gather.ensure(std::max(words, per * (size_t)g) * 8));
+  uint64_t* rbuf = static_cast<uint64_t*>(root.gather.p);
+  // (an injected fault stops here, before the group: a group that some ranks
+  // join and others do not would never complete)
+  STL_RCCL_TRY(g_rccl.GroupStart());
+  int rc = STL_OK;
+  for (int r = 0; r < g && rc == STL_OK; ++r) {
+    Device& d = *sh[r].d;
+    const uint64_t* sbuf = static_cast<const uint64_t*>(d.bitmap.p);
+    if (equal) {
+      if (g_rccl.Gather(sbuf, rbuf, per, ncclUint64, 0, d.comm, d.stream) != ncclSuccess) rc = STL_ERCCL;
+    } else {
+      const size_t w = (sh[r].hi - sh[r].lo + 63) / 64;
+      if (w == 0 || r == 0) continue;  // rank 0's own slice: a device copy below
+      if (g_rccl.Send(sbuf, w, ncclUint64, 0, d.comm, d.stream) != ncclSuccess ||
+          g_rccl.Recv(rbuf + sh[r].lo / 64, w, ncclUint64, r, root.comm, root.stream) != ncclSuccess)
+        rc = STL_ERCCL;
+    }
+  }
+  if (g_rccl.GroupEnd() != ncclSuccess && rc == STL_OK) rc = STL_ERCCL;
   if (rc) return rc;
-  const uint32_t policy = stl::kernel_mode(flags);
+  STL_TRY(hipSetDevice(root.ordinal));
+  if (!equal && sh[0].hi > sh[0].lo)
+    STL_TRY(hipMemcpyAsync(rbuf, root.bitmap.p, (sh[0].hi - sh[0].lo + 63) / 64 * 8, hipMemcpyDeviceToDevice,
+                           root.stream));
+  std::vector<uint8_t> host_words(words * 8);
+  STL_TRY(hipMemcpyAsync(host_words.data(), rbuf, words * 8, hipMemcpyDeviceToHost, root.stream));
+  STL_TRY(hipStreamSynchronize(root.stream));
+  std::memcpy(b.bitmap, host_words.data(), (n + 7) / 8);
+  return STL_OK;
+}
+
+int check_flags(uint32_t flags) {
+  return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) ? STL_EINVAL : STL_OK;
+}
+
+int run_batch(const Batch& b, size_t n) {
+  if (n == 0) return STL_OK;
+  STL_RC(ensure_init());
   const int g = (int)g_devs.size();
   if (g == 0) return STL_ENODEV;
   // one kernel launch handles up to 2^32-64 signatures per shard
   const size_t kMaxShard = (size_t)1 << 31;
-  int gg = (int)std::max<size_t>((size_t)g, (n + kMaxShard - 1) / kMaxShard);
-  std::vector<int> rcs(gg, STL_OK);
-  std::vector<std::thread> th;
+  int gg = g * g_shards_per_device;
+  while ((n + gg - 1) / gg > kMaxShard) gg += g;
+  std::vector<size_t> bound;
+  const bool by_bytes = b.mode != Mode::kSig && gg > 1;
+  if (by_bytes) shard_bytes_bounds(b.len, n, gg, bound);
+  std::vector<Shard> sh(gg);
   for (int r = 0; r < gg; ++r) {
-    size_t lo, hi;
-    shard(n, r, gg, &lo, &hi);
-    Device& d = *g_devs[r % g];
-    if (gg == 1) {
-      rcs[r] = run_shard(d, sig, msg32, pk, pre, off, len, lo, hi, bitmap, policy);
+    sh[r].d = g_devs[r % g].get();
+    if (by_bytes) {
+      sh[r].lo = bound[r];
+      sh[r].hi = bound[r + 1];
     } else {
-      th.emplace_back([&, r, lo, hi]() { rcs[r] = run_shard(*g_devs[r % g], sig, msg32, pk, pre, off, len, lo, hi, bitmap, policy); });
+      shard(n, r, gg, &sh[r].lo, &sh[r].hi);
     }
   }
+  if (g_comm_gather && gg == g) {
+    // RCCL path: every device's mutex for the whole batch (device order)
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (auto& d : g_devs) locks.emplace_back(d->mu);
+    size_t per = 1;
+    for (auto& s : sh) per = std::max(per, (s.hi - s.lo + 63) / 64);
+    std::vector<std::thread> th;
+    for (int r = 0; r < gg; ++r) {
+      if (r + 1 == gg) sh[r].rc = enqueue_shard(b, sh[r], per);
+      else th.emplace_back([&, r] { sh[r].rc = enqueue_shard(b, sh[r], per); });
+    }
+    for (auto& t : th) t.join();
+    int rc = STL_OK;
+    for (auto& s : sh) rc = rc ? rc : s.rc;
+    if (rc == STL_OK) rc = gather_to_host(b, sh, n, per, !by_bytes);
+    for (auto& d : g_devs) {
+      const int drc = drain(*d);
+      rc = rc ? rc : drc;
+    }
+    return rc;
+  }
+  std::vector<std::thread> th;
+  for (int r = 0; r < gg; ++r) {
+    if (r + 1 == gg) sh[r].rc = run_shard_direct(b, sh[r]);
+    else th.emplace_back([&, r] { sh[r].rc = run_shard_direct(b, sh[r]); });
+  }
   for (auto& t : th) t.join();
-  for (int r : rcs)
-    if (r) return r;
+  for (auto& s : sh)
+    if (s.rc) return s.rc;
   return STL_OK;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
 }
 
 }  // namespace
@@ -336,51 +535,76 @@ extern "C" {
 int stl_init(const stl_config* cfg) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_init) return STL_OK;
-  int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return STL_ENODEV;
-  int first = 0, want = count;
-  if (cfg) {
-    if (cfg->struct_size != sizeof(stl_config)) return STL_EINVAL;
+  const char* fa = std::getenv("STL_FAULT_AFTER");
+  if (fa && *fa) g_fault_after.store(std::atoll(fa));
+  int first = 0, want = -1, spd = 1;
+  uint32_t cflags = 0;
+  if (cfg) {  // argument checks first: they need no device
+    const uint32_t abi1 = 4 * sizeof(uint32_t);
+    if (cfg->struct_size != sizeof(stl_config) && cfg->struct_size != abi1) return STL_EINVAL;
     first = cfg->first_device;
     if (cfg->device_count > 0) want = cfg->device_count;
+    cflags = cfg->flags;
+    if ((cflags & ~(STL_CFG_RCCL_GATHER | STL_CFG_NO_RCCL)) ||
+        (cflags & (STL_CFG_RCCL_GATHER | STL_CFG_NO_RCCL)) == (STL_CFG_RCCL_GATHER | STL_CFG_NO_RCCL) ||
+        first < 0)
+      return STL_EINVAL;
+    if (cfg->struct_size == sizeof(stl_config)) {
+      if (cfg->reserved != 0) return STL_EINVAL;
+      if (cfg->shards_per_device > 0) spd = cfg->shards_per_device;
+    }
   }
-  if (const char* env = std::getenv("STL_DEVICES")) want = std::max(1, std::atoi(env));
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return STL_ENODEV;
+  if (want < 0) want = count;
+  if (std::getenv("STL_DEVICES")) want = std::max(1, env_int("STL_DEVICES", want));
+  spd = std::max(1, std::min(64, env_int("STL_SHARDS_PER_DEVICE", spd)));
+  const int env_rccl = env_int("STL_RCCL", -1);
+  if (env_rccl == 1) cflags = (cflags & ~STL_CFG_NO_RCCL) | STL_CFG_RCCL_GATHER;
+  if (env_rccl == 0) cflags = (cflags & ~STL_CFG_RCCL_GATHER) | STL_CFG_NO_RCCL;
   if (first < 0 || first >= count) return STL_EINVAL;
   want = std::min(want, count - first);
   int prev = 0;
   (void)hipGetDevice(&prev);
+  auto fail = [&](int rc) {
+    for (auto& d : g_devs) release_device(*d);
+    g_devs.clear();
+    (void)hipSetDevice(prev);
+    return rc;
+  };
   for (int i = 0; i < want; ++i) {
     std::unique_ptr<Device> d(new Device());
     d->ordinal = first + i;
-    int rc = setup_device(*d);
-    if (rc) {
-      (void)hipSetDevice(prev);
-      g_devs.clear();
-      return rc;
-    }
     g_devs.push_back(std::move(d));
+    const int rc = setup_device(*g_devs.back());
+    if (rc) return fail(rc);
+  }
+  const bool gather = !(cflags & STL_CFG_NO_RCCL) && spd == 1 && (want >= 2 || (cflags & STL_CFG_RCCL_GATHER));
+  if (gather) {
+    if (!g_rccl.load() || fault_now()) return fail(STL_ERCCL);
+    std::vector<ncclComm_t> comms(want);
+    std::vector<int> ords(want);
+    for (int i = 0; i < want; ++i) ords[i] = g_devs[i]->ordinal;
+    if (g_rccl.CommInitAll(comms.data(), want, ords.data()) != ncclSuccess) return fail(STL_ERCCL);
+    for (int i = 0; i < want; ++i) g_devs[i]->comm = comms[i];
   }
   (void)hipSetDevice(prev);
+  g_shards_per_device = spd;
+  g_comm_gather = gather;
   g_init = true;
   return STL_OK;
 }
 
 void stl_shutdown(void) {
+  stl_comm_destroy();
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& d : g_devs) {
     std::lock_guard<std::mutex> dl(d->mu);
-    (void)hipSetDevice(d->ordinal);
-    (void)hipStreamSynchronize(d->stream);
-    for (DevBuf* b : {&d->ws, &d->sig, &d->msg, &d->pk, &d->bitmap, &d->pre, &d->off, &d->len, &d->ctr, &d->txid,
-                      &d->status, &d->wide})
-      b->release();
-    for (auto& kv : d->stream_ws) kv.second->release();
-    for (auto& kv : d->stream_ctr) kv.second->release();
-    (void)hipStreamSynchronize(d->copy);
-    (void)hipStreamDestroy(d->stream);
-    (void)hipStreamDestroy(d->copy);
+    release_device(*d);
   }
   g_devs.clear();
+  g_comm_gather = false;
+  g_shards_per_device = 1;
   g_init = false;
 }
 
@@ -389,7 +613,7 @@ int stl_device_count(void) {
   return (int)g_devs.size();
 }
 
-const char* stl_version(void) { return "stl 0.1.0 (gfx950, abi 1)"; }
+const char* stl_version(void) { return "stl 0.2.0 (gfx950, abi 2)"; }
 
 const char* stl_strerror(int rc) {
   switch (rc) {
@@ -398,105 +622,156 @@ const char* stl_strerror(int rc) {
     case STL_ENODEV: return "no gfx950 device";
     case STL_ENOMEM: return "out of memory";
     case STL_EHIP: return "HIP runtime error";
+    case STL_ERCCL: return "RCCL error";
     default: return "unknown error";
   }
 }
 
+void stl_debug_fault_after(long long calls) { g_fault_after.store(calls < 0 ? -1 : calls); }
+
+void stl_shard_range(size_t n, int r, int g, size_t* lo, size_t* hi) {
+  if (!lo || !hi) return;
+  if (g < 1 || r < 0 || r >= g) {
+    *lo = *hi = n;
+    return;
+  }
+  shard(n, r, g, lo, hi);
+}
+
+void stl_shard_range_bytes(const uint32_t* len, size_t n, int r, int g, size_t* lo, size_t* hi) {
+  if (!lo || !hi) return;
+  if (g < 1 || r < 0 || r >= g || (n && !len)) {
+    *lo = *hi = n;
+    return;
+  }
+  std::vector<size_t> bound;
+  shard_bytes_bounds(len, n, g, bound);
+  *lo = bound[r];
+  *hi = bound[r + 1];
+}
+
 int stl_ed25519_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
                              uint8_t* accept_bitmap, uint32_t flags) {
-  if (n && !msg) return STL_EINVAL;
-  return run_batch(sig, msg, pk, nullptr, nullptr, nullptr, n, accept_bitmap, flags);
+  if (n == 0) return STL_OK;
+  if (!sig || !msg || !pk || !accept_bitmap) return STL_EINVAL;
+  STL_RC(check_flags(flags));
+  const Batch b{Mode::kSig, sig, msg, pk, nullptr, nullptr, nullptr, accept_bitmap, nullptr, nullptr,
+                stl::kernel_mode(flags), 0u};
+  return run_batch(b, n);
 }
 
 int stl_tx_verify_batch(const uint8_t* preimages, const uint64_t* offset, const uint32_t* len, const uint8_t* sig,
                         const uint8_t* pk, size_t n, uint8_t* accept_bitmap, uint32_t flags) {
-  return run_batch(sig, nullptr, pk, preimages, offset, len, n, accept_bitmap, flags);
+  if (n == 0) return STL_OK;
+  if (!preimages || !offset || !len || !sig || !pk || !accept_bitmap) return STL_EINVAL;
+  STL_RC(check_flags(flags));
+  const Batch b{Mode::kPre, sig, nullptr, pk, preimages, offset, len, accept_bitmap, nullptr, nullptr,
+                stl::kernel_mode(flags), 0u};
+  return run_batch(b, n);
+}
+
+int stl_signed_blob_verify_batch(uint32_t kind, const uint8_t* blobs, const uint64_t* offset, const uint32_t* len,
+                                 size_t n, uint8_t* accept_bitmap, uint8_t* status, uint8_t* id, uint32_t flags) {
+  if (kind != STL_BLOB_TRANSACTION && kind != STL_BLOB_VALIDATION) return STL_EINVAL;
+  if (n == 0) return STL_OK;
+  if (!blobs || !offset || !len || !accept_bitmap) return STL_EINVAL;
+  STL_RC(check_flags(flags));
+  const Batch b{Mode::kBlob, nullptr, nullptr, nullptr, blobs, offset, len, accept_bitmap, status, id,
+                stl::kernel_mode(flags), kind};
+  return run_batch(b, n);
 }
 
 int stl_tx_blob_verify_batch(const uint8_t* blobs, const uint64_t* offset, const uint32_t* len, size_t n,
                              uint8_t* accept_bitmap, uint8_t* status, uint8_t* tx_id, uint32_t flags) {
-  if (n == 0) return STL_OK;
-  if (!blobs || !offset || !len || !accept_bitmap) return STL_EINVAL;
-  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) return STL_EINVAL;
-  int rc = ensure_init();
-  if (rc) return rc;
-  const uint32_t policy = stl::kernel_mode(flags);
-  const int g = (int)g_devs.size();
-  if (g == 0) return STL_ENODEV;
-  const size_t kMaxShard = (size_t)1 << 31;
-  const int gg = (int)std::max<size_t>((size_t)g, (n + kMaxShard - 1) / kMaxShard);
-  std::vector<int> rcs(gg, STL_OK);
-  std::vector<std::thread> th;
-  for (int r = 0; r < gg; ++r) {
-    size_t lo, hi;
-    shard(n, r, gg, &lo, &hi);
-    if (gg == 1) {
-      rcs[r] = run_blob_shard(*g_devs[0], blobs, offset, len, lo, hi, accept_bitmap, status, tx_id, policy);
-    } else {
-      th.emplace_back([&, r, lo, hi]() {
-        rcs[r] = run_blob_shard(*g_devs[r % g], blobs, offset, len, lo, hi, accept_bitmap, status, tx_id, policy);
-      });
-    }
-  }
-  for (auto& t : th) t.join();
-  for (int r : rcs)
-    if (r) return r;
-  return STL_OK;
+  return stl_signed_blob_verify_batch(STL_BLOB_TRANSACTION, blobs, offset, len, n, accept_bitmap, status, tx_id,
+                                      flags);
 }
 
 int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned long long mlen, const uint8_t* pk) {
   if (!sig || !pk || (mlen && !m)) return STL_EINVAL;
   if (mlen == 32) {
     uint8_t bit = 0;
-    int rc = stl_ed25519_verify_batch(sig, m, pk, 1, &bit, STL_POLICY_SODIUM_1_0_18);
+    const int rc = stl_ed25519_verify_batch(sig, m, pk, 1, &bit, STL_POLICY_SODIUM_1_0_18);
     if (rc) return rc;
     return (bit & 1) ? 0 : -1;
   }
+  if (mlen > 0xffffffffull) return STL_EINVAL;
   // arbitrary-length message: k = H(R||A||m) mod L on the device, then verify
-  int rc = ensure_init();
-  if (rc) return rc;
+  STL_RC(ensure_init());
   Device& d = *g_devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
   STL_TRY(hipSetDevice(d.ordinal));
-  if ((rc = d.ws.ensure(stl::verify_ws_bytes(d.grid))) || (rc = d.sig.ensure(64)) || (rc = d.pk.ensure(32)) ||
-      (rc = d.msg.ensure(32)) || (rc = d.bitmap.ensure(8)) || (rc = d.pre.ensure(mlen ? mlen : 1)) ||
-      (rc = d.off.ensure(16)))
-    return rc;
+  STL_RC(d.ws.ensure(stl::verify_ws_bytes(d.grid)));
+  STL_RC(d.sig.ensure(64));
+  STL_RC(d.pk.ensure(32));
+  STL_RC(d.msg.ensure(32));
+  STL_RC(d.bitmap.ensure(8));
+  STL_RC(d.pre.ensure(mlen ? mlen : 1));
+  STL_RC(d.off.ensure(16));
   hipStream_t s = d.stream;
   const uint64_t hostmeta[2] = {0, mlen};
-  STL_TRY(hipMemcpyAsync(d.sig.p, sig, 64, hipMemcpyHostToDevice, s));
-  STL_TRY(hipMemcpyAsync(d.pk.p, pk, 32, hipMemcpyHostToDevice, s));
-  if (mlen) STL_TRY(hipMemcpyAsync(d.pre.p, m, mlen, hipMemcpyHostToDevice, s));
-  STL_TRY(hipMemcpyAsync(d.off.p, hostmeta, 16, hipMemcpyHostToDevice, s));
-  uint64_t* meta = static_cast<uint64_t*>(d.off.p);
-  STL_TRY(stl::launch_hram_var(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.pk.p),
-                               static_cast<uint8_t*>(d.pre.p), meta, meta + 1, 1, static_cast<uint8_t*>(d.msg.p), s));
-  STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
-                             static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
-                             STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true,
-                             static_cast<const uint4*>(d.wide.p), s));
   uint64_t word = 0;
-  STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
-  STL_TRY(hipStreamSynchronize(s));
+  auto enqueue = [&]() -> int {
+    STL_TRY(hipMemcpyAsync(d.sig.p, sig, 64, hipMemcpyHostToDevice, s));
+    STL_TRY(hipMemcpyAsync(d.pk.p, pk, 32, hipMemcpyHostToDevice, s));
+    if (mlen) STL_TRY(hipMemcpyAsync(d.pre.p, m, mlen, hipMemcpyHostToDevice, s));
+    STL_TRY(hipMemcpyAsync(d.off.p, hostmeta, 16, hipMemcpyHostToDevice, s));
+    uint64_t* meta = static_cast<uint64_t*>(d.off.p);
+    STL_TRY(stl::launch_hram_var(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.pk.p),
+                                 static_cast<uint8_t*>(d.pre.p), meta, meta + 1, 1, static_cast<uint8_t*>(d.msg.p), s));
+    STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
+                               static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
+                               STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true,
+                               static_cast<const uint4*>(d.wide.p), s));
+    STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
+    STL_TRY(hipStreamSynchronize(s));
+    return STL_OK;
+  };
+  const int rc = enqueue();
+  const int drc = drain(d);
+  if (rc || drc) return rc ? rc : drc;
   return (word & 1) ? 0 : -1;
 }
+
+namespace {
+int device_for_call(Device** out) {
+  STL_RC(ensure_init());
+  const int di = current_device_index();
+  if (di < 0) return STL_ENODEV;
+  *out = g_devs[di].get();
+  return STL_OK;
+}
+}  // namespace
 
 int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, const uint8_t* d_pk, size_t n,
                                     uint64_t* d_bitmap_words, uint32_t flags, void* stream) {
   if (n == 0) return STL_OK;
   if (!d_sig || !d_msg || !d_pk || !d_bitmap_words) return STL_EINVAL;
-  if (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) return STL_EINVAL;
+  STL_RC(check_flags(flags));
   if (n > 0xffffffc0ull) return STL_EINVAL;
-  int rc = ensure_init();
-  if (rc) return rc;
-  const int di = current_device_index();
-  if (di < 0) return STL_ENODEV;
-  Device& d = *g_devs[di];
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint4* ws = nullptr;
-  if ((rc = stream_workspace(d, s, &ws))) return rc;
+  STL_RC(stream_workspace(*d, s, &ws));
   STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(d, n), false, static_cast<const uint4*>(d.wide.p), s));
+                             grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s));
+  return STL_OK;
+}
+
+int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const uint8_t* d_pk, size_t n,
+                              uint64_t* d_bitmap_words, uint32_t flags, void* stream) {
+  if (n == 0) return STL_OK;
+  if (!d_sig || !d_k || !d_pk || !d_bitmap_words) return STL_EINVAL;
+  STL_RC(check_flags(flags));
+  if (n > 0xffffffc0ull) return STL_EINVAL;
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint4* ws = nullptr;
+  STL_RC(stream_workspace(*d, s, &ws));
+  STL_TRY(stl::launch_verify(d_sig, d_k, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
+                             grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s));
   return STL_OK;
 }
 
@@ -504,50 +779,99 @@ int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offse
                              uint8_t* d_msg, void* stream) {
   if (n == 0) return STL_OK;
   if (!d_preimages || !d_offset || !d_len || !d_msg || n > 0xffffffc0ull) return STL_EINVAL;
-  int rc = ensure_init();
-  if (rc) return rc;
-  const int di = current_device_index();
-  if (di < 0) return STL_ENODEV;
-  Device& d = *g_devs[di];
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t* ctr = nullptr;
-  if ((rc = stream_queue(d, s, n, &ctr))) return rc;
-  STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(d), s));
+  STL_RC(stream_queue(*d, s, n, &ctr));
+  STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(*d), s));
+  return STL_OK;
+}
+
+int stl_signed_blob_prepare_device(uint32_t kind, const uint8_t* d_blobs, const uint64_t* d_offset,
+                                   const uint32_t* d_len, size_t n, uint8_t* d_msg, uint8_t* d_sig, uint8_t* d_pk,
+                                   uint8_t* d_id, uint8_t* d_status, void* stream) {
+  if (kind != STL_BLOB_TRANSACTION && kind != STL_BLOB_VALIDATION) return STL_EINVAL;
+  if (n == 0) return STL_OK;
+  if (!d_blobs || !d_offset || !d_len || !d_msg || !d_sig || !d_pk || !d_status || n > 0xffffffc0ull)
+    return STL_EINVAL;
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* ctr = nullptr;
+  STL_RC(stream_queue(*d, s, n, &ctr));
+  STL_TRY(stl::launch_tx_blob(d_blobs, d_offset, d_len, (uint32_t)n, d_msg, d_sig, d_pk, d_id, d_status, ctr,
+                              hash_grid(*d), s, kind));
   return STL_OK;
 }
 
 int stl_tx_blob_prepare_device(const uint8_t* d_blobs, const uint64_t* d_offset, const uint32_t* d_len, size_t n,
                                uint8_t* d_msg, uint8_t* d_sig, uint8_t* d_pk, uint8_t* d_tx_id, uint8_t* d_status,
                                void* stream) {
-  if (n == 0) return STL_OK;
-  if (!d_blobs || !d_offset || !d_len || !d_msg || !d_sig || !d_pk || !d_status || n > 0xffffffc0ull)
-    return STL_EINVAL;
-  int rc = ensure_init();
-  if (rc) return rc;
-  const int di = current_device_index();
-  if (di < 0) return STL_ENODEV;
-  Device& d = *g_devs[di];
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  uint32_t* ctr = nullptr;
-  if ((rc = stream_queue(d, s, n, &ctr))) return rc;
-  STL_TRY(stl::launch_tx_blob(d_blobs, d_offset, d_len, (uint32_t)n, d_msg, d_sig, d_pk, d_tx_id, d_status, ctr,
-                              hash_grid(d), s));
-  return STL_OK;
+  return stl_signed_blob_prepare_device(STL_BLOB_TRANSACTION, d_blobs, d_offset, d_len, n, d_msg, d_sig, d_pk,
+                                        d_tx_id, d_status, stream);
 }
 
 int stl_ed25519_sign_batch_device(const uint8_t* d_seed, const uint8_t* d_msg, size_t n, uint8_t* d_pk,
                                   uint8_t* d_sig, void* stream) {
   if (n == 0) return STL_OK;
   if (!d_seed || !d_msg || !d_pk || !d_sig || n > 0xffffffc0ull) return STL_EINVAL;
-  int rc = ensure_init();
-  if (rc) return rc;
-  const int di = current_device_index();
-  if (di < 0) return STL_ENODEV;
-  Device& d = *g_devs[di];
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint4* ws = nullptr;
-  if ((rc = stream_workspace(d, s, &ws))) return rc;
-  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, ws, grid_for(d, n), s));
+  STL_RC(stream_workspace(*d, s, &ws));
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, ws, grid_for(*d, n), s));
+  return STL_OK;
+}
+
+// ---- one process per GPU ----------------------------------------------------
+
+int stl_comm_unique_id(uint8_t id[128]) {
+  if (!id) return STL_EINVAL;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  if (!g_rccl.load()) return STL_ERCCL;
+  ncclUniqueId u;
+  STL_RCCL_TRY(g_rccl.GetUniqueId(&u));
+  std::memcpy(id, &u, sizeof u);
+  return STL_OK;
+}
+
+int stl_comm_init_rank(int nranks, int rank, const uint8_t id[128]) {
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) return STL_EINVAL;
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
+  if (!g_rccl.load()) return STL_ERCCL;
+  std::lock_guard<std::mutex> lk(g_pcomm_mu);
+  if (g_pcomm) return STL_EINVAL;  // one communicator per process; stl_comm_destroy first
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  ncclComm_t c = nullptr;
+  STL_RCCL_TRY(g_rccl.CommInitRank(&c, nranks, u, rank));
+  g_pcomm = c;
+  g_pcomm_ranks = nranks;
+  return STL_OK;
+}
+
+void stl_comm_destroy(void) {
+  std::lock_guard<std::mutex> lk(g_pcomm_mu);
+  if (g_pcomm && g_rccl.ok) (void)g_rccl.CommDestroy(g_pcomm);
+  g_pcomm = nullptr;
+  g_pcomm_ranks = 0;
+}
+
+int stl_bitmap_gather_device(const uint64_t* d_words, size_t words_per_rank, uint64_t* d_all_words, int root,
+                             void* stream) {
+  std::lock_guard<std::mutex> lk(g_pcomm_mu);
+  if (!g_pcomm) return STL_ERCCL;
+  if (!d_words || words_per_rank == 0 || root >= g_pcomm_ranks) return STL_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (root < 0) {
+    if (!d_all_words) return STL_EINVAL;
+    STL_RCCL_TRY(g_rccl.AllGather(d_words, d_all_words, words_per_rank, ncclUint64, g_pcomm, s));
+  } else {
+    STL_RCCL_TRY(g_rccl.Gather(d_words, d_all_words, words_per_rank, ncclUint64, root, g_pcomm, s));
+  }
   return STL_OK;
 }
 

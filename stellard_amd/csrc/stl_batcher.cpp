@@ -13,7 +13,12 @@
 // Verdicts: STL_VERDICT_ACCEPT / STL_VERDICT_REJECT, STL_VERDICT_DEFER for a
 // serialized transaction the device did not decide (its status
 // STL_TX_DEFERRED), or a negative STL_E* code when the device batch failed --
-// the caller then runs its own check (never a reject).
+// the caller then runs its own check (never a reject).  A batch starts when
+// max_batch requests of one kind are pending or the OLDEST pending request has
+// waited max_delay_us (each request keeps its arrival time, so leftovers from
+// a full batch are not delayed again).  Callbacks run on the worker thread and
+// must not call stl_batcher_flush / stl_batcher_destroy on their aggregator.
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -32,12 +37,14 @@ struct SigReq {
   uint8_t sig[64], msg[32], pk[32];
   stl_verdict_fn fn;
   void* ctx;
+  Clock::time_point arrival;
 };
 
 struct TxReq {
   std::vector<uint8_t> blob;
   stl_verdict_fn fn;
   void* ctx;
+  Clock::time_point arrival;
 };
 
 }  // namespace
@@ -48,14 +55,21 @@ struct stl_batcher {
   uint32_t flags = 0;
   std::mutex mu;
   std::condition_variable cv_work, cv_done;
-  std::vector<SigReq> sigs;
-  std::vector<TxReq> txs;
-  Clock::time_point oldest;  // arrival of the oldest pending request
+  std::deque<SigReq> sigs;
+  std::deque<TxReq> txs;
   uint64_t submitted = 0, completed = 0, batches = 0;
-  bool flushing = false, stop = false;
+  uint64_t flush_target = 0;  // flush() callers wait for completed >= this
+  bool stop = false;
   std::thread worker;
 
   size_t pending() const { return sigs.size() + txs.size(); }
+  bool flushing() const { return completed < flush_target; }
+  // arrival of the oldest pending request (each queue is in arrival order)
+  Clock::time_point oldest() const {
+    if (sigs.empty()) return txs.front().arrival;
+    if (txs.empty()) return sigs.front().arrival;
+    return std::min(sigs.front().arrival, txs.front().arrival);
+  }
 
   void run() {
     std::unique_lock<std::mutex> lk(mu);
@@ -65,37 +79,28 @@ struct stl_batcher {
         cv_work.wait(lk, [&] { return stop || pending() > 0; });
         continue;
       }
-      const bool full = pending() >= max_batch;
-      if (!full && !flushing && !stop) {
-        const auto deadline = oldest + max_delay;
+      const bool full = sigs.size() >= max_batch || txs.size() >= max_batch;
+      if (!full && !flushing() && !stop) {
+        // deadline of the oldest pending request: requests left over from a
+        // previous round keep their own arrival time
+        const auto deadline = oldest() + max_delay;
         if (Clock::now() < deadline) {
           cv_work.wait_until(lk, deadline);
           continue;
         }
       }
-      std::vector<SigReq> s;
-      std::vector<TxReq> t;
-      // take at most max_batch of each kind; the rest stays for the next round
-      if (sigs.size() > max_batch) {
-        s.assign(sigs.begin(), sigs.begin() + max_batch);
-        sigs.erase(sigs.begin(), sigs.begin() + max_batch);
-      } else {
-        s.swap(sigs);
-      }
-      if (txs.size() > max_batch) {
-        t.assign(std::make_move_iterator(txs.begin()), std::make_move_iterator(txs.begin() + max_batch));
-        txs.erase(txs.begin(), txs.begin() + max_batch);
-      } else {
-        t.swap(txs);
-      }
-      oldest = Clock::now();
+      // take at most max_batch of each kind, oldest first; the rest stays
+      const size_t ns = std::min<size_t>(sigs.size(), max_batch), nt = std::min<size_t>(txs.size(), max_batch);
+      std::vector<SigReq> s(sigs.begin(), sigs.begin() + ns);
+      std::vector<TxReq> t(std::make_move_iterator(txs.begin()), std::make_move_iterator(txs.begin() + nt));
+      sigs.erase(sigs.begin(), sigs.begin() + ns);
+      txs.erase(txs.begin(), txs.begin() + nt);
       lk.unlock();
       run_sigs(s);
       run_txs(t);
       lk.lock();
       completed += s.size() + t.size();
       batches += (s.empty() ? 0 : 1) + (t.empty() ? 0 : 1);
-      if (pending() == 0) flushing = false;
       cv_done.notify_all();
     }
   }
@@ -142,10 +147,8 @@ struct stl_batcher {
   }
 
   void note_arrival() {
-    if (pending() == 1) oldest = Clock::now();
     ++submitted;
-    if (pending() >= max_batch) cv_work.notify_one();
-    else if (pending() == 1) cv_work.notify_one();
+    if (pending() == 1 || sigs.size() >= max_batch || txs.size() >= max_batch) cv_work.notify_one();
   }
 };
 
@@ -158,7 +161,6 @@ stl_batcher* stl_batcher_create(uint32_t max_batch, uint32_t max_delay_us, uint3
   b->max_batch = max_batch;
   b->max_delay = std::chrono::microseconds(max_delay_us);
   b->flags = flags;
-  b->oldest = Clock::now();
   b->worker = std::thread([b] { b->run(); });
   return b;
 }
@@ -172,6 +174,7 @@ int stl_batcher_submit(stl_batcher* b, const uint8_t* sig, const uint8_t* msg32,
   std::memcpy(r.pk, pk, 32);
   r.fn = fn;
   r.ctx = ctx;
+  r.arrival = Clock::now();
   std::lock_guard<std::mutex> lk(b->mu);
   if (b->stop) return STL_EINVAL;
   b->sigs.push_back(r);
@@ -185,6 +188,7 @@ int stl_batcher_submit_tx(stl_batcher* b, const uint8_t* blob, size_t len, stl_v
   r.blob.assign(blob, blob + len);
   r.fn = fn;
   r.ctx = ctx;
+  r.arrival = Clock::now();
   std::lock_guard<std::mutex> lk(b->mu);
   if (b->stop) return STL_EINVAL;
   b->txs.push_back(std::move(r));
@@ -196,7 +200,7 @@ void stl_batcher_flush(stl_batcher* b) {
   if (!b) return;
   std::unique_lock<std::mutex> lk(b->mu);
   const uint64_t target = b->submitted;
-  b->flushing = true;
+  b->flush_target = std::max(b->flush_target, target);  // cleared by itself once completed >= target
   b->cv_work.notify_one();
   b->cv_done.wait(lk, [&] { return b->completed >= target; });
 }

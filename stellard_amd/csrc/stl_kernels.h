@@ -40,7 +40,7 @@ hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_
                           uint32_t* qws, uint32_t grid, hipStream_t stream);
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
-                          hipStream_t stream);
+                          hipStream_t stream, uint32_t kind = 0u /* STL_BLOB_* */);
 // Wide base tables (stl_verify_core.h): 2 * 32769 rows of 28 words.
 constexpr size_t kWideTableBytes = 2ull * 32769 * 28 * 4;
 hipError_t launch_wide_table(uint4* out, hipStream_t stream);

@@ -460,15 +460,17 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
                                                          uint8_t* __restrict__ msg, uint8_t* __restrict__ sig,
                                                          uint8_t* __restrict__ pk, uint8_t* __restrict__ txid,
                                                          uint8_t* __restrict__ status, uint32_t* __restrict__ counter,
-                                                         const uint32_t* __restrict__ order) {
+                                                         const uint32_t* __restrict__ order, BlobKind kind) {
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
-  SpliceStream ss;  // phase 0: "STX\0" || blob minus the cut fields
-  ByteStream bs;    // phase 1: the 4 bytes before the blob || blob, word 0 -> "TXN\0"
-  ss.init(blobs, 0, kPrefixTxSign, nullptr);
+  SpliceStream ss;  // phase 0: sign prefix || blob minus the cut fields
+  ByteStream bs;    // phase 1: [the 4 bytes before the blob, word 0 -> id prefix] || blob
+  ss.init(blobs, 0, kind.sign_prefix, nullptr);
   bs.init(blobs, 0);
-  const uint32_t txn_le = bswap32(kPrefixTxId);
+  const uint32_t txn_le = bswap32(kind.id_prefix);
+  const bool id_pfx = kind.id_prefixed != 0;
+  const uint32_t pfx_bytes = id_pfx ? 4u : 0u;
   uint64_t st[8];
   sha512_init(st);
   uint32_t mi = 0, blk = 0, nb = 0, phase = 0;
@@ -491,7 +493,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
           const uint32_t L = len[mi];
           bend = b + L;
           TxLayout t;
-          tx_blob_parse(b, L, t);
+          tx_blob_parse(b, L, t, kind.sig_code, kind.min_len);
           status[mi] = (uint8_t)t.status;
           uint4* sq = reinterpret_cast<uint4*>(sig + 64 * (size_t)mi);
           if (t.status == kTxOk) {
@@ -503,7 +505,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
             sq[2] = make_uint4(sgw[8], sgw[9], sgw[10], sgw[11]);
             sq[3] = make_uint4(sgw[12], sgw[13], sgw[14], sgw[15]);
             st8(pk + 32 * (size_t)mi, pkw);
-            ss.init(b, L, kPrefixTxSign, &t);
+            ss.init(b, L, kind.sign_prefix, &t);
             nb = ss.blocks();
             phase = 0;
           } else {
@@ -513,7 +515,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
             pq[0] = z; pq[1] = z;
             uint4* mq = reinterpret_cast<uint4*>(msg + 32 * (size_t)mi);
             mq[0] = z; mq[1] = z;
-            bs.init(b - 4, L + 4);
+            bs.init(b - pfx_bytes, L + pfx_bytes);
             nb = bs.blocks();
             phase = 1;
           }
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
         ss.block(w, blk, blk + 1 == nb, src);
       } else {
         block_from_window(w, lw, (uint32_t)(blk_addr & 15u) >> 2, bs.mis, (int32_t)bs.len - (int32_t)(128 * blk),
-                          blk + 1 == nb, bs.len, blk == 0, true, txn_le);
+                          blk + 1 == nb, bs.len, blk == 0, id_pfx, txn_le);
       }
       sha512_compress(st, w);
       if (++blk == nb) {
@@ -557,7 +559,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
         if (phase == 0) {
           st8(msg + 32 * (size_t)mi, h);
           if (txid != nullptr) {
-            bs.init(b - 4, len[mi] + 4);
+            bs.init(b - pfx_bytes, len[mi] + pfx_bytes);
             nb = bs.blocks();
             blk = 0;
             sha512_init(st);
@@ -671,7 +673,8 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   uint4* slots = ws;
   uint4* pre = ws + (size_t)grid * (kWsBytesPerBlock / 16);
   uint64_t* fb = reinterpret_cast<uint64_t*>(pre + (size_t)kPreChunk * 14);
-  for (uint32_t base = 0; base < n; base += kPreChunk) {
+  for (uint64_t b64 = 0; b64 < n; b64 += kPreChunk) {  // 64-bit: n may reach 2^32 - 64
+    const uint32_t base = (uint32_t)b64;
     const uint32_t cnt = n - base < kPreChunk ? n - base : kPreChunk;
     const dim3 g1((cnt + kBlock - 1) / kBlock);
     const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
@@ -728,13 +731,14 @@ hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_
 
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
-                          hipStream_t stream) {
+                          hipStream_t stream, uint32_t kind_id) {
   if (n == 0) return hipSuccess;
-  hipError_t e = launch_order(len, n, 4u, qws, stream);
+  const BlobKind kind = kind_id == 1u ? blob_kind_validation() : blob_kind_tx();
+  hipError_t e = launch_order(len, n, kind.id_prefixed ? 4u : 0u, qws, stream);
   if (e != hipSuccess) return e;
   const uint32_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(tx_blob_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, blobs, off, len,
-                     n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4);
+                     n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4, kind);
   return hipGetLastError();
 }
 

@@ -44,8 +44,10 @@ namespace stl {
 
 constexpr uint32_t kPrefixTxSign = 0x53545800u;  // HashPrefix::txSign "STX\0", HashPrefix.cpp:30
 constexpr uint32_t kPrefixTxId = 0x54584E00u;    // HashPrefix::transactionID "TXN\0", HashPrefix.cpp:25
+constexpr uint32_t kPrefixValidation = 0x56414C00u;  // HashPrefix::validation "VAL\0", HashPrefix.cpp:31
 constexpr uint32_t kTxMinBytes = 32;             // Protocol::txMinSizeBytes
 constexpr uint32_t kTxMaxBytes = 1024 * 1024;    // Protocol::txMaxSizeBytes
+constexpr uint32_t kValMinBytes = 50;            // PeerImp::recvValidation, PeerImp.cpp:1134
 constexpr int kBlobMaxDepth = 8;
 
 // per-transaction status (include/stl.h STL_TX_*)
@@ -61,6 +63,23 @@ constexpr uint32_t kCodeSignature = 0x70006u;      // VL 6
 constexpr uint32_t kCodeTxnSignatures = 0xF0003u;  // ARRAY 3
 constexpr uint32_t kCodeObjectEnd = 0xE0001u;      // STI_OBJECT, 1
 constexpr uint32_t kCodeArrayEnd = 0xF0001u;       // STI_ARRAY, 1
+
+// Which signed object a blob is (include/stl.h STL_BLOB_*): the signing-hash
+// prefix, the field that holds the signature, and the ID hash.
+struct BlobKind {
+  uint32_t sign_prefix;  // getSigningHash prefix
+  uint32_t sig_code;     // signature field (SigningPubKey is VL 3 for both)
+  uint32_t id_prefix;    // ID = SHA512Half(id_prefix || blob), or of the blob alone
+  uint32_t id_prefixed;  // 0: no prefix
+  uint32_t min_len;
+};
+// SerializedTransaction: checkSign / getTransactionID (SerializedTransaction.cpp:162-171,220-230)
+STL_HD BlobKind blob_kind_tx() { return BlobKind{kPrefixTxSign, kCodeTxnSignature, kPrefixTxId, 1u, kTxMinBytes}; }
+// SerializedValidation::isValid (SerializedValidation.cpp:70-73,96-110); ID =
+// the suppression hash SHA512Half(raw validation), PeerImp.cpp:1148-1155
+STL_HD BlobKind blob_kind_validation() {
+  return BlobKind{kPrefixValidation, kCodeSignature, 0u, 0u, kValMinBytes};
+}
 
 STL_HD uint64_t name_range(int a, int b) { return ((2ull << b) - 1ull) & ~((1ull << a) - 1ull); }
 
@@ -109,7 +128,7 @@ STL_HD uint32_t fixed_size(uint32_t type) {
 struct TxLayout {
   uint32_t status;
   uint32_t pk_off, pk_len;    // SigningPubKey payload (pk_len 0xffffffff: absent)
-  uint32_t sig_off, sig_len;  // TxnSignature payload
+  uint32_t sig_off, sig_len;  // signature payload (TxnSignature; Signature for validations)
   uint32_t xs0, xe0, xs1, xe1, xs2, xe2;
 };
 
@@ -121,12 +140,13 @@ STL_HD bool bytes_nonzero(const uint8_t* b, uint32_t pos, uint32_t n) {
 
 // The canonical-form pass over one blob (one lane).  Byte loads only: fields
 // are short and the pass is a few percent of the hashing that follows.
-STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t) {
+STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t, uint32_t sig_code = kCodeTxnSignature,
+                          uint32_t min_len = kTxMinBytes) {
   t.status = kTxDeferred;
   t.pk_off = t.sig_off = 0;
   t.pk_len = t.sig_len = 0xffffffffu;
   t.xs0 = t.xe0 = t.xs1 = t.xe1 = t.xs2 = t.xe2 = len;
-  if (len < kTxMinBytes || len > kTxMaxBytes) return;
+  if (len < min_len || len > kTxMaxBytes) return;
   uint32_t last[kBlobMaxDepth + 1];
   last[0] = 0;
   uint32_t arrays = 0;  // bit d: level d is an array
@@ -212,7 +232,7 @@ STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t) {
       if (depth == 0 && code == kCodeSigningPubKey) {
         t.pk_off = pos;
         t.pk_len = size;
-      } else if (depth == 0 && code == kCodeTxnSignature) {
+      } else if (depth == 0 && code == sig_code) {
         t.sig_off = pos;
         t.sig_len = size;
       }

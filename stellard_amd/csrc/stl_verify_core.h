@@ -63,9 +63,20 @@ STL_HD bool point_is_canonical(const uint32_t s[8]) {
   return !(top && s[0] >= 0xffffffedu);
 }
 
-// Pre-checks of crypto_sign_verify_detached for the selected policy.
+STL_HD bool all_zero(const uint32_t s[8]) {
+  uint32_t a = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a |= s[i];
+  return a == 0;
+}
+
+// Pre-checks of crypto_sign_verify_detached for the selected policy.  The
+// 1.0.0 policy also rejects the all-zero key, as some 1.0.x releases did (it
+// decodes to a point of order 4, for which signatures can be forged).  That
+// case is parity-unpinned offline and a reject is the
+// safe side: stellard then runs its own serial check.
 STL_HD bool verify_prechecks(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], uint32_t policy) {
-  if (policy == kPolicyStellard100) return (S[7] >> 29) == 0;  // sig[63] & 224
+  if (policy == kPolicyStellard100) return (S[7] >> 29) == 0 && !all_zero(A);  // sig[63] & 224
   return sc_lt_L(S) && !has_small_order(R) && point_is_canonical(A) && !has_small_order(A);
 }
 

@@ -18,6 +18,34 @@ def shard_range(n, rank, world):
     return lo, hi
 
 
+def shard_range_bytes(lens, rank, world):
+    """Byte-balanced shard (same as stl_api.cpp shard_bytes_bounds /
+    stl_shard_range_bytes): boundary r is the 64-aligned row at or after the
+    first row where the byte prefix sum reaches r/world of the total.
+    Variable-length rows (config 5: 100 B - 4 KB preimages) cost in
+    proportion to their SHA-512 blocks, so ranks get equal bytes, not equal
+    counts."""
+    lens = np.asarray(lens, dtype=np.uint64)
+    n = lens.shape[0]
+
+    def bound(r):
+        if r <= 0:
+            return 0
+        if r >= world:
+            return n
+        total = int(lens.sum())
+        target = total * r // world
+        csum = np.cumsum(lens, dtype=np.uint64)
+        # smallest i with prefix(i) = sum(lens[:i]) >= target
+        i = 0 if target == 0 else int(np.searchsorted(csum, target, side="left")) + 1
+        return min(n, (i + 63) // 64 * 64)
+
+    b = [bound(0)]
+    for r in range(1, world + 1):
+        b.append(max(b[-1], bound(r)))
+    return b[rank], b[rank + 1]
+
+
 def words_per_rank(n, world):
     return ((n + 63) // 64 + world - 1) // world
 
@@ -32,6 +60,27 @@ def gather_bitmap_words(local_words, n, world, dist, group=None):
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
     return torch.cat(parts)[: (n + 63) // 64]
+
+
+def gather_bitmap_words_v(local_words, bounds, dist, group=None):
+    """Gather for unequal (byte-balanced) shards: rank r holds the words of
+    rows [bounds[r], bounds[r+1]) (every bound a multiple of 64 or the end).
+    Pads every slice to the largest, all-gathers, and places slice r at word
+    bounds[r] // 64.  The same placement libstl's grouped send/recv gather
+    uses (stl_api.cpp gather_to_host)."""
+    import torch
+    world = len(bounds) - 1
+    n = bounds[-1]
+    per = max(1, max((bounds[r + 1] - bounds[r] + 63) // 64 for r in range(world)))
+    buf = torch.zeros(per, dtype=torch.int64, device=local_words.device)
+    buf[: local_words.numel()] = local_words
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    out = torch.zeros((n + 63) // 64, dtype=torch.int64, device=local_words.device)
+    for r in range(world):
+        w = (bounds[r + 1] - bounds[r] + 63) // 64
+        out[bounds[r] // 64: bounds[r] // 64 + w] = parts[r][:w]
+    return out
 
 
 def words_to_bool(words, n):

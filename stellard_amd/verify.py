@@ -33,12 +33,37 @@ def _buf(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def init(device_count=0, first_device=0):
-    class Cfg(ctypes.Structure):
-        _fields_ = [("struct_size", ctypes.c_uint32), ("device_count", ctypes.c_int32),
-                    ("first_device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
-    cfg = Cfg(ctypes.sizeof(Cfg), device_count, first_device, 0)
+class Config(ctypes.Structure):
+    """stl_config (include/stl.h, ABI 2)."""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device_count", ctypes.c_int32),
+                ("first_device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("shards_per_device", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
+def init(device_count=0, first_device=0, flags=0, shards_per_device=1):
+    """stl_init (sodium_init's place, ripple_app.cpp:129-132).  flags:
+    N.STL_CFG_RCCL_GATHER / N.STL_CFG_NO_RCCL."""
+    cfg = Config(ctypes.sizeof(Config), device_count, first_device, flags, shards_per_device, 0)
     return N.check(N.load().stl_init(ctypes.byref(cfg)), "stl_init")
+
+
+def shutdown():
+    N.load().stl_shutdown()
+
+
+def shard_range(n, rank, world):
+    """stl_shard_range: contiguous 64-aligned index shard of rank r."""
+    lo, hi = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    N.load().stl_shard_range(n, rank, world, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+def shard_range_bytes(lens, rank, world):
+    """stl_shard_range_bytes: byte-balanced 64-aligned shard of rank r."""
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    lo, hi = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    N.load().stl_shard_range_bytes(_buf(lens), lens.shape[0], rank, world, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
 
 
 def verify_signature(hash32, sig, pk):
@@ -112,6 +137,26 @@ def _pack(chunks):
 TX_OK, TX_DEFERRED, TX_MALFORMED = N.STL_TX_OK, N.STL_TX_DEFERRED, N.STL_TX_MALFORMED
 
 
+BLOB_TRANSACTION, BLOB_VALIDATION = N.STL_BLOB_TRANSACTION, N.STL_BLOB_VALIDATION
+
+
+def signed_blob_verify_batch(blobs, kind=BLOB_TRANSACTION, policy=POLICY_SODIUM_1_0_18, ids=False):
+    """stl_signed_blob_verify_batch: the signature check of serialized signed
+    objects (list of bytes).  kind BLOB_TRANSACTION = checkSign,
+    BLOB_VALIDATION = SerializedValidation::isValid.  Returns (accept bool[n],
+    status uint8[n]) plus the IDs (n, 32) when ``ids``."""
+    n = len(blobs)
+    buf, offs, lens = _pack(blobs)
+    bitmap = np.zeros((n + 7) // 8 or 1, dtype=np.uint8)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    idb = np.zeros((max(n, 1), 32), dtype=np.uint8) if ids else None
+    N.check(N.load().stl_signed_blob_verify_batch(kind, _buf(buf), _buf(offs), _buf(lens), n, _buf(bitmap),
+                                                  _buf(status), _buf(idb) if ids else None, policy),
+            "stl_signed_blob_verify_batch")
+    bits = unpack_bitmap(bitmap, n)
+    return (bits, status[:n], idb[:n]) if ids else (bits, status[:n])
+
+
 def tx_blob_verify_batch(blobs, policy=POLICY_SODIUM_1_0_18, tx_ids=False):
     """checkSign straight from serialized transactions (list of bytes, each
     the whole transaction with its TxnSignature).  Returns (accept bool[n],
@@ -126,6 +171,17 @@ def tx_blob_verify_batch(blobs, policy=POLICY_SODIUM_1_0_18, tx_ids=False):
                                               _buf(ids) if tx_ids else None, policy), "stl_tx_blob_verify_batch")
     bits = unpack_bitmap(bitmap, n)
     return (bits, status[:n], ids[:n]) if tx_ids else (bits, status[:n])
+
+
+def proposal_preimage(propose_seq, close_time, prev_ledger, position):
+    """LedgerProposal::getSigningHash preimage (LedgerProposal.cpp:54-65):
+    "PRP\0" || seq || closeTime (big-endian u32, Serializer::add32) ||
+    previous ledger || position (uint256 bytes, add256); 76 bytes."""
+    prev_ledger, position = bytes(prev_ledger), bytes(position)
+    if len(prev_ledger) != 32 or len(position) != 32:
+        raise ValueError("ledger hashes are 32 bytes")
+    return (b"PRP\x00" + int(propose_seq).to_bytes(4, "big") + int(close_time).to_bytes(4, "big")
+            + prev_ledger + position)
 
 
 # ---- transaction level: SerializedTransaction::checkSign ----
@@ -222,7 +278,7 @@ def verify_batch_device(sig, msg, pk, out_words=None, policy=POLICY_SODIUM_1_0_1
     return out_words
 
 
-def tx_blob_prepare_device(blobs, offsets, lengths, tx_ids=True, stream=None):
+def tx_blob_prepare_device(blobs, offsets, lengths, tx_ids=True, stream=None, kind=None):
     """Serialized transactions already in HBM (uint8 / int64 / int32 CUDA
     tensors) -> dict of msg (n,32), sig (n,64), pk (n,32), status (n,) and
     tx_id (n,32) tensors, asynchronously on ``stream``; follow with
@@ -241,9 +297,10 @@ def tx_blob_prepare_device(blobs, offsets, lengths, tx_ids=True, stream=None):
     if offsets.dtype != torch.int64 or lengths.dtype != torch.int32:
         raise ValueError("offsets must be int64 and lengths int32")
     ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-    N.check(N.load().stl_tx_blob_prepare_device(
-        ptr(blobs), ptr(offsets), ptr(lengths), n, ptr(out["msg"]), ptr(out["sig"]), ptr(out["pk"]),
-        ptr(out["tx_id"]), ptr(out["status"]), _stream_ptr(stream)), "stl_tx_blob_prepare_device")
+    N.check(N.load().stl_signed_blob_prepare_device(
+        N.STL_BLOB_TRANSACTION if kind is None else kind, ptr(blobs), ptr(offsets), ptr(lengths), n,
+        ptr(out["msg"]), ptr(out["sig"]), ptr(out["pk"]), ptr(out["tx_id"]), ptr(out["status"]),
+        _stream_ptr(stream)), "stl_signed_blob_prepare_device")
     return out
 
 
@@ -323,6 +380,55 @@ class Batcher:
 
 
 VERDICT_REJECT, VERDICT_ACCEPT, VERDICT_DEFER = N.STL_VERDICT_REJECT, N.STL_VERDICT_ACCEPT, N.STL_VERDICT_DEFER
+
+
+# ---- one process per GPU: the RCCL bitmap gather (include/stl.h) ----
+
+def comm_unique_id():
+    """stl_comm_unique_id: 128 bytes for rank 0 to hand to every rank."""
+    buf = ctypes.create_string_buffer(128)
+    N.check(N.load().stl_comm_unique_id(buf), "stl_comm_unique_id")
+    return buf.raw
+
+
+def comm_init_rank(nranks, rank, uid):
+    uid = bytes(uid)
+    if len(uid) != 128:
+        raise ValueError("unique id is 128 bytes")
+    N.check(N.load().stl_comm_init_rank(nranks, rank, uid), "stl_comm_init_rank")
+
+
+def comm_destroy():
+    N.load().stl_comm_destroy()
+
+
+def bitmap_gather_device(words, out_words=None, root=0, stream=None):
+    """stl_bitmap_gather_device: every rank's int64 bitmap words (CUDA tensor of
+    words_per_rank words) into out_words (nranks*words_per_rank) on rank
+    ``root`` (root < 0: all ranks)."""
+    ptr = ctypes.c_void_p(out_words.data_ptr()) if out_words is not None else None
+    N.check(N.load().stl_bitmap_gather_device(ctypes.c_void_p(words.data_ptr()), words.numel(), ptr, root,
+                                              _stream_ptr(stream)), "stl_bitmap_gather_device")
+    return out_words
+
+
+# ---- testing hooks ----
+
+def debug_fault_after(calls):
+    """stl_debug_fault_after: the HIP/RCCL call after ``calls`` more fails (one shot)."""
+    N.load().stl_debug_fault_after(calls)
+
+
+def debug_verify_k_device(sig, k, pk, out_words=None, policy=POLICY_SODIUM_1_0_18, stream=None):
+    """stl_debug_verify_k_device: verify with given k (n,32) instead of hashing."""
+    import torch
+    n = sig.shape[0]
+    if out_words is None:
+        out_words = torch.empty((n + 63) // 64, dtype=torch.int64, device=sig.device)
+    N.check(N.load().stl_debug_verify_k_device(
+        ctypes.c_void_p(sig.data_ptr()), ctypes.c_void_p(k.data_ptr()), ctypes.c_void_p(pk.data_ptr()), n,
+        ctypes.c_void_p(out_words.data_ptr()), policy, _stream_ptr(stream)), "stl_debug_verify_k_device")
+    return out_words
 
 
 def sign_batch_device(seed, msg, stream=None):

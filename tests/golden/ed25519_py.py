@@ -147,7 +147,9 @@ def verify(sig, msg, pk, policy="1.0.18"):
         if S >= L or has_small_order(R) or not is_canonical_point(pk) or has_small_order(pk):
             return False
     else:
-        if sig[63] & 0xE0:
+        # 1.0.0: only the top 3 bits of S; the all-zero key is rejected too (as
+        # some 1.0.x releases did; unpinned offline, the conservative side)
+        if sig[63] & 0xE0 or bytes(pk) == bytes(32):
             return False
     A = decode(pk)
     if A is None:

@@ -162,6 +162,28 @@ void hostemu_tx_blob(const uint8_t* blob, uint32_t len, uint32_t* status, uint8_
   std::memcpy(layout, l, sizeof l);
 }
 
+// The same pass for either signed-object kind (0 transaction, 1 validation,
+// stl_txblob.h BlobKind): status, signing hash, ID.
+void hostemu_signed_blob(uint32_t kind, const uint8_t* blob, uint32_t len, uint32_t* status, uint8_t msg[32],
+                         uint8_t id[32]) {
+  const stl::BlobKind k = kind == 1 ? stl::blob_kind_validation() : stl::blob_kind_tx();
+  stl::TxLayout t;
+  stl::tx_blob_parse(blob, len, t, k.sig_code, k.min_len);
+  *status = t.status;
+  uint32_t h[8];
+  std::memset(msg, 0, 32);
+  std::memset(id, 0, 32);
+  if (t.status == stl::kTxOk) {
+    stl::splice_sha512_half(h, blob, len, k.sign_prefix, &t);
+    std::memcpy(msg, h, 32);
+  }
+  if (t.status != stl::kTxDeferred) {
+    if (k.id_prefixed) stl::splice_sha512_half(h, blob, len, k.id_prefix, nullptr);
+    else stl::sha512_half_words(h, blob, len);
+    std::memcpy(id, h, 32);
+  }
+}
+
 // block_from_window (the hash kernels' assembly from an LDS window) against
 // ByteStream::block for a message at buf+off of length len: every block,
 // optionally with the 4-byte prefix form.  Returns the number of differing

@@ -49,6 +49,11 @@ class Oracle:
         lib.oracle_tx_blob.restype = ctypes.c_int
         lib.oracle_tx_blob.argtypes = [V, ctypes.c_size_t, V, V, ctypes.c_size_t, ctypes.POINTER(TxInfo)]
         lib.oracle_tx_blob_verify_batch.argtypes = [V, V, V, ctypes.c_size_t, V, V, ctypes.c_uint32, ctypes.c_int]
+        lib.oracle_signed_blob.restype = ctypes.c_int
+        lib.oracle_signed_blob.argtypes = [ctypes.c_uint32, V, ctypes.c_size_t, V, V, ctypes.c_size_t,
+                                           ctypes.POINTER(TxInfo)]
+        lib.oracle_signed_blob_verify_batch.argtypes = [ctypes.c_uint32, V, V, V, ctypes.c_size_t, V, V,
+                                                        ctypes.c_uint32, ctypes.c_int]
 
     def verify(self, sig, msg, pk, policy=0):
         return self.lib.oracle_verify(bytes(sig), bytes(msg), len(msg), bytes(pk), policy) == 0
@@ -101,6 +106,26 @@ class Oracle:
         rc = self.lib.oracle_tx_blob(bytes(blob), len(blob), s, f, cap, ctypes.byref(info))
         return rc == 0, info, s.raw[:info.signing_len], f.raw[:info.full_len]
 
+    def signed_blob(self, kind, blob):
+        """Reference deserialise + re-serialise of one signed object (kind 0
+        transaction, 1 validation): (ok, info, signing, full)."""
+        cap = len(blob) + 64
+        s = ctypes.create_string_buffer(cap)
+        f = ctypes.create_string_buffer(cap)
+        info = TxInfo()
+        rc = self.lib.oracle_signed_blob(kind, bytes(blob), len(blob), s, f, cap, ctypes.byref(info))
+        return rc == 0, info, s.raw[:info.signing_len], f.raw[:info.full_len]
+
+    def signed_blob_verify_batch(self, kind, blobs, policy=0, threads=0, ids=False):
+        buf, offs, lens = pack_blobs(blobs)
+        n = len(blobs)
+        bm = np.zeros((n + 7) // 8 or 1, np.uint8)
+        idb = np.zeros((max(n, 1), 32), np.uint8)
+        self.lib.oracle_signed_blob_verify_batch(kind, _buf(buf), _buf(offs), _buf(lens), n, _buf(bm),
+                                                 _buf(idb) if ids else None, policy, threads)
+        bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+        return (bits, idb[:n]) if ids else bits
+
     def tx_blob_verify_batch(self, blobs, policy=0, threads=0, tx_ids=False):
         buf, offs, lens = pack_blobs(blobs)
         n = len(blobs)
@@ -143,6 +168,8 @@ def load_sodium_ref():
     lib.ref_seed_keypair.argtypes = [V, V, V]
     lib.ref_sign_detached.argtypes = [V, V, ctypes.c_ulonglong, V]
     lib.ref_tx_blob_verify_batch.argtypes = [V, V, V, ctypes.c_size_t, V, V, ctypes.c_uint32, ctypes.c_int]
+    lib.ref_signed_blob_verify_batch.argtypes = [ctypes.c_uint32, V, V, V, ctypes.c_size_t, V, V, ctypes.c_uint32,
+                                                 ctypes.c_int]
     if lib.ref_init() != 0:
         return None
     return lib
@@ -167,6 +194,27 @@ def sodium_tx_blob_verify_batch(lib, blobs, threads=0, tx_ids=False):
                                  0, threads)
     bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
     return (bits, ids[:n]) if tx_ids else bits
+
+
+def sodium_signed_blob_verify_batch(lib, kind, blobs, threads=0, ids=False):
+    buf, offs, lens = pack_blobs(blobs)
+    n = len(blobs)
+    bm = np.zeros((n + 7) // 8 or 1, np.uint8)
+    idb = np.zeros((max(n, 1), 32), np.uint8)
+    lib.ref_signed_blob_verify_batch(kind, _buf(buf), _buf(offs), _buf(lens), n, _buf(bm),
+                                     _buf(idb) if ids else None, 0, threads)
+    bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    return (bits, idb[:n]) if ids else bits
+
+
+def hostemu_signed_blob(lib, kind, blob):
+    """Device pass (either kind) compiled for the host: (status, msg, id)."""
+    st = ctypes.c_uint32(0)
+    msg = ctypes.create_string_buffer(32)
+    idb = ctypes.create_string_buffer(32)
+    arr = np.frombuffer(bytes(blob) + b"\0" * 4, np.uint8).copy()
+    lib.hostemu_signed_blob(kind, _buf(arr), len(blob), ctypes.byref(st), msg, idb)
+    return st.value, msg.raw, idb.raw
 
 
 def hostemu_tx_blob(lib, blob):
@@ -197,6 +245,7 @@ def load_hostemu():
     lib.hostemu_sc_mul_signed.argtypes = [V, ctypes.c_int, V, V]
     lib.hostemu_sha512_half.argtypes = [V, ctypes.c_uint32, V]
     lib.hostemu_tx_blob.argtypes = [V, ctypes.c_uint32, V, V, V, V]
+    lib.hostemu_signed_blob.argtypes = [ctypes.c_uint32, V, ctypes.c_uint32, V, V, V]
     lib.hostemu_blob_words.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, V]
     lib.hostemu_wide_row.argtypes = [ctypes.c_int, ctypes.c_uint32, V]
     lib.hostemu_window_blocks.restype = ctypes.c_uint32

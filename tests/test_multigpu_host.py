@@ -1,0 +1,202 @@
+"""Multi-GPU plumbing on CPU (no GPU needed):
+
+* bench.py --gpus N is a launcher: it starts N ranks as child processes
+  (torch.distributed.run) and the ranks report n_gpus = N; --dry-run runs the
+  ranks' control plane and bitmap gather over gloo without a GPU;
+* libstl's shard functions (stl_shard_range / stl_shard_range_bytes, which
+  the host batch calls and the RCCL gather use) equal the Python mirror;
+* byte-balanced shards of variable-length rows (config 5) over 2 gloo ranks
+  reassemble exactly the single-rank bitmap (oracle as the per-rank checker:
+  this box has no GPU);
+* stl_init checks its configuration before it looks for a device.
+Reference parallelism being replaced: the JobQueue thread pool,
+src/ripple_core/functional/JobQueue.cpp:217-243."""
+import ctypes
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from stellard_amd import shard
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _last_json(out):
+    for line in reversed(out.strip().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError(f"no JSON line in output:\n{out}")
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_launcher_dry_run(gpus):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dry-run",
+                        "--steps", "2", "--warmup", "1", "--per-gpu", "4160"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == gpus and line["dry_run"] is True
+    assert line["steps"] == 2 and line["warmup"] == 1 and line["scaling"] == "weak"
+    assert line["config"]["gathered_all_ones"] is True
+    assert line["config"]["rank0_shard"] == [0, 4160]
+    assert line["metric"].startswith("DRY RUN")
+
+
+def test_bench_rank_count_must_match():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "one rank per GPU" in (r.stdout + r.stderr)
+
+
+def _c_shard(lib, n, r, g):
+    lo, hi = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    lib.stl_shard_range(n, r, g, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+def _c_shard_bytes(lib, lens, r, g):
+    lens = np.ascontiguousarray(lens, np.uint32)
+    lo, hi = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    lib.stl_shard_range_bytes(lens.ctypes.data_as(ctypes.c_void_p), lens.shape[0], r, g, ctypes.byref(lo),
+                              ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+def test_c_shards_equal_python_mirror():
+    from stellard_amd import _native
+    lib = _native.load()
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 63, 64, 65, 1000, 4097, 1 << 20, 67108864):
+        for g in (1, 2, 3, 4, 7, 8):
+            for r in range(g):
+                assert _c_shard(lib, n, r, g) == shard.shard_range(n, r, g)
+    for trial in range(60):
+        n = int(rng.integers(0, 5000))
+        g = int(rng.integers(1, 9))
+        if trial % 3 == 0:
+            lens = np.exp(rng.uniform(np.log(100), np.log(4096), n)).astype(np.uint32)  # config 5 shape
+        elif trial % 3 == 1:
+            lens = rng.integers(0, 3, n).astype(np.uint32)  # zeros and tiny rows
+        else:
+            lens = np.where(rng.random(n) < 0.01, 1 << 20, 113).astype(np.uint32)  # a few huge rows
+        for r in range(g):
+            assert _c_shard_bytes(lib, lens, r, g) == shard.shard_range_bytes(lens, r, g), (n, g, r)
+
+
+def test_byte_shards_cover_align_and_balance():
+    rng = np.random.default_rng(6)
+    lens = np.exp(rng.uniform(np.log(100), np.log(4096), 200000)).astype(np.uint32)
+    total = int(lens.sum())
+    for g in (2, 4, 8):
+        b = [shard.shard_range_bytes(lens, r, g) for r in range(g)]
+        assert b[0][0] == 0 and b[-1][1] == lens.shape[0]
+        for (lo, hi), (lo2, _) in zip(b, b[1:]):
+            assert hi == lo2 and lo % 64 == 0
+        per = [int(lens[lo:hi].sum()) for lo, hi in b]
+        # every shard within one 64-row word of bytes of the ideal split
+        assert max(abs(p - total / g) for p in per) <= 2 * 64 * 4096
+        # whereas equal-count shards of a length-sorted batch are badly skewed
+    srt = np.sort(lens)
+    b = [shard.shard_range_bytes(srt, r, 2) for r in range(2)]
+    assert b[0][1] > srt.shape[0] // 2  # more short rows in the first shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tx_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from tests import oracle_bind, txblob
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = oracle_bind.load_oracle()
+    blobs, pres = txblob.valid_corpus(o, 300, 11, with_preimages=True)
+    rng = np.random.default_rng(12)
+    lens = np.array([len(b) for b in blobs], np.uint32)
+    bounds = [shard.shard_range_bytes(lens, r, world)[0] for r in range(world)] + [len(blobs)]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    bad = rng.random(len(blobs)) < 0.3
+    blobs = [b[:-1] + bytes([b[-1] ^ 1]) if x else b for b, x in zip(blobs, bad)]
+    bits = o.tx_blob_verify_batch(blobs[lo:hi], threads=2)
+    full = shard.gather_bitmap_words_v(torch.from_numpy(shard.bool_to_words(bits)), bounds, dist)
+    if rank == 0:
+        ref = o.tx_blob_verify_batch(blobs, threads=2)
+        q.put((shard.words_to_bool(full, len(blobs)).tolist(), ref.tolist(), [lo, hi]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_byte_shards_reassemble_tx_bitmap():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tx_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, ref, rank0 = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == ref
+    assert 0 < rank0[1] < 300 and rank0[1] % 64 == 0
+
+
+class Cfg(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device_count", ctypes.c_int32),
+                ("first_device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("shards_per_device", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
+def test_init_checks_config_before_devices():
+    import torch
+    from stellard_amd import _native as N
+    lib = N.load()
+    sz = ctypes.sizeof(Cfg)
+    assert sz == 24
+    bad = [Cfg(20, 0, 0, 0, 1, 0), Cfg(sz, 0, 0, N.STL_CFG_RCCL_GATHER | N.STL_CFG_NO_RCCL, 1, 0),
+           Cfg(sz, 0, 0, 0x80, 1, 0), Cfg(sz, 0, -1, 0, 1, 0), Cfg(sz, 0, 0, 0, 1, 7)]
+    for c in bad:
+        assert lib.stl_init(ctypes.byref(c)) == N.STL_EINVAL
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: the valid configurations are exercised by the gpu tests")
+    for c in (Cfg(sz, 0, 0, 0, 3, 0), Cfg(16, 0, 0, 0, 0, 0), Cfg(sz, 2, 0, N.STL_CFG_RCCL_GATHER, 1, 0)):
+        assert lib.stl_init(ctypes.byref(c)) == N.STL_ENODEV
+    assert lib.stl_comm_init_rank(2, 0, bytes(128)) == N.STL_ENODEV
+    assert lib.stl_bitmap_gather_device(None, 1, None, 0, None) == N.STL_ERCCL  # no communicator
+
+
+def test_batcher_flush_with_nothing_pending_keeps_the_delay():
+    """stl_batcher_flush on an idle aggregator must not make the next request
+    skip its max_delay wait (the old flag stayed set)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    from stellard_amd import verify as V
+    with V.Batcher(max_batch=64, max_delay_us=400_000) as b:
+        b.flush()
+        t0 = time.perf_counter()
+        h = b.submit(bytes(64), bytes(32), bytes(32))
+        v = h.result(timeout=10)
+        waited = time.perf_counter() - t0
+        assert v < 0
+        assert waited >= 0.3, waited

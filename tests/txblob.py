@@ -36,6 +36,12 @@ Memos = (ARRAY, 9)
 TxnSignatures = (ARRAY, 3)
 Template = (ARRAY, 5)
 TakerPaysCurrency = (HASH160, 1)
+# SerializedValidation's template (SerializedValidation.cpp:134-159)
+LedgerSequence, CloseTime, SigningTime = (UINT32, 6), (UINT32, 7), (UINT32, 9)
+LoadFee, ReserveBase, ReserveIncrement = (UINT32, 24), (UINT32, 31), (UINT32, 32)
+BaseFee = (UINT64, 5)
+LedgerHash = (HASH256, 1)
+Amendments = (VECTOR256, 3)
 
 NON_SIGNING = {TxnSignature, Signature, TxnSignatures}
 
@@ -198,6 +204,45 @@ def signed_blob(fields, sk, signer):
 
 def tx_id(blob):
     return sha512_half(b"TXN\x00" + bytes(blob))
+
+
+def validation_fields(rng, pk, *, full=True, extras=True):
+    """A SerializedValidation's fields (SerializedValidation.cpp:39-56,
+    134-159): Flags (vfFullyCanonicalSig 0x80000000, kFullFlag 0x1),
+    LedgerHash, SigningTime, SigningPubKey, optional LedgerSequence /
+    CloseTime / LoadFee / Amendments / BaseFee / Reserve*."""
+    fs = [Field(Flags, u32(0x80000000 | (1 if full else 0))),
+          Field(LedgerHash, rng.bytes(32)),
+          Field(SigningTime, u32(int(rng.integers(0, 2**32)))),
+          Field(SigningPubKey, vl(pk))]
+    if extras:
+        if rng.random() < 0.7:
+            fs.append(Field(LedgerSequence, u32(int(rng.integers(1, 2**31)))))
+        if rng.random() < 0.5:
+            fs.append(Field(CloseTime, u32(int(rng.integers(0, 2**32)))))
+        if rng.random() < 0.3:
+            fs.append(Field(LoadFee, u32(int(rng.integers(256, 2**16)))))
+        if rng.random() < 0.2:
+            fs.append(Field(Amendments, vl(rng.bytes(32 * int(rng.integers(1, 4))))))
+        if rng.random() < 0.2:
+            fs.append(Field(BaseFee, int(rng.integers(1, 2**40)).to_bytes(8, "big")))
+            fs.append(Field(ReserveBase, u32(int(rng.integers(1, 2**31)))))
+            fs.append(Field(ReserveIncrement, u32(int(rng.integers(1, 2**31)))))
+    return fs
+
+
+def validation_preimage(fields):
+    """STObject::getSigningHash(SIGN_VALIDATION) preimage: "VAL\0" || fields
+    without Signature (SerializedValidation.cpp:70-73, HashPrefix.cpp:31)."""
+    return b"VAL\x00" + serialize(fields, skip=NON_SIGNING)
+
+
+def signed_validation(fields, sk, signer):
+    """SerializedValidation::sign (SerializedValidation.cpp:59-68): sign the
+    signing hash, set sfSignature; returns (blob, signing hash, signature)."""
+    h = sha512_half(validation_preimage(fields))
+    sig = signer(h, sk)
+    return serialize(fields + [Field(Signature, vl(sig))]), h, sig
 
 
 # ------------------------------------------------------------- corpora
