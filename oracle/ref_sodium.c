@@ -127,3 +127,44 @@ void ref_tx_verify_batch(const uint8_t *pre, const uint64_t *off, const uint32_t
   job_t p = {sig, NULL, pk, pre, off, len, 0, 0, NULL};
   run(p, n, bitmap, threads);
 }
+
+/* Synthetic data for the committed bitmap digests (tests/golden/make_digests.py):
+ * keypair from seed_i (crypto_sign_seed_keypair, EdKeyPair::setSeed,
+ * EdKeyPair.cpp:25-33) and a detached signature over the 32-byte msg_i
+ * (RippleAddress::sign, RippleAddress.cpp:254-263).  RFC 8032 signing is
+ * deterministic, so the GPU signer reproduces these bytes on the box. */
+typedef struct {
+  const uint8_t *seed, *msg;
+  uint8_t *pk, *sig;
+  size_t lo, hi;
+} sign_job_t;
+
+static void *sign_worker(void *arg) {
+  sign_job_t *j = (sign_job_t *)arg;
+  unsigned char sk[64];
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    crypto_sign_seed_keypair(j->pk + 32 * i, sk, j->seed + 32 * i);
+    crypto_sign_detached(j->sig + 64 * i, NULL, j->msg + 32 * i, 32, sk);
+  }
+  sodium_memzero(sk, sizeof sk);
+  return NULL;
+}
+
+void ref_sign_batch(const uint8_t *seed, const uint8_t *msg, size_t n, uint8_t *pk, uint8_t *sig, int threads) {
+  if (threads <= 0) threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  if (threads > 512) threads = 512;
+  if ((size_t)threads > n) threads = n ? (int)n : 1;
+  pthread_t tid[512];
+  sign_job_t jobs[512];
+  size_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].seed = seed;
+    jobs[t].msg = msg;
+    jobs[t].pk = pk;
+    jobs[t].sig = sig;
+    jobs[t].lo = (size_t)t * chunk < n ? (size_t)t * chunk : n;
+    jobs[t].hi = jobs[t].lo + chunk < n ? jobs[t].lo + chunk : n;
+    pthread_create(&tid[t], NULL, sign_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+}

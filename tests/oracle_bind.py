@@ -168,6 +168,7 @@ def load_sodium_ref():
     lib.ref_seed_keypair.argtypes = [V, V, V]
     lib.ref_sign_detached.argtypes = [V, V, ctypes.c_ulonglong, V]
     lib.ref_tx_blob_verify_batch.argtypes = [V, V, V, ctypes.c_size_t, V, V, ctypes.c_uint32, ctypes.c_int]
+    lib.ref_sign_batch.argtypes = [V, V, ctypes.c_size_t, V, V, ctypes.c_int]
     lib.ref_signed_blob_verify_batch.argtypes = [ctypes.c_uint32, V, V, V, ctypes.c_size_t, V, V, ctypes.c_uint32,
                                                  ctypes.c_int]
     if lib.ref_init() != 0:
@@ -194,6 +195,17 @@ def sodium_tx_blob_verify_batch(lib, blobs, threads=0, tx_ids=False):
                                  0, threads)
     bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
     return (bits, ids[:n]) if tx_ids else bits
+
+
+def sodium_sign_batch(lib, seeds, msgs, threads=0):
+    """libsodium keypair(seed_i) + detached signature over msg_i (32 B)."""
+    seeds = np.ascontiguousarray(seeds, np.uint8)
+    msgs = np.ascontiguousarray(msgs, np.uint8)
+    n = seeds.shape[0]
+    pk = np.empty((n, 32), np.uint8)
+    sig = np.empty((n, 64), np.uint8)
+    lib.ref_sign_batch(_buf(seeds), _buf(msgs), n, _buf(pk), _buf(sig), threads)
+    return pk, sig
 
 
 def sodium_signed_blob_verify_batch(lib, kind, blobs, threads=0, ids=False):

@@ -1,0 +1,68 @@
+"""GPU parity at BASELINE.json's full sizes, pinned by committed data:
+libstl's accept bitmaps for the seeded datasets of configs 2 (1,048,576
+signatures), 4 (10,000,000, 2 % adversarial rows of every Appendix-B class)
+and 3 (67,108,864, same construction) against the SHA-256 digests of the
+bitmaps libsodium 1.0.18 gave the same rows (tests/golden/bitmap_digests.json,
+made by tests/golden/make_digests.py in the build container).  The inputs are
+regenerated here with the GPU signer (RFC 8032 signing is deterministic; the
+input digest checks that) -- nothing from libsodium is needed on the box.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120
+"""
+import json
+import time
+
+import numpy as np
+import pytest
+
+from tests import datasets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def stl(torch_cuda):
+    from stellard_amd import verify
+    verify.init()
+    return verify
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name", ["config2", "config4", "config3"])
+def test_config_bitmap_digest(stl, torch_cuda, name):
+    torch = torch_cuda
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)[name]
+    pool = datasets.adversarial_pool()
+
+    def sign(seeds, msgs):
+        pk, sig = stl.sign_batch_device(torch.from_numpy(seeds).cuda(), torch.from_numpy(msgs).cuda())
+        return pk.cpu().numpy(), sig.cpu().numpy()
+
+    dg = datasets.Digest()
+    t0, gpu_s = time.time(), 0.0
+    for c0, seed, n, frac in datasets.chunks(name):
+        sig, msg, pk, _ = datasets.chunk(seed, n, frac, sign, pool)
+        d = [torch.from_numpy(a).cuda() for a in (sig, msg, pk)]
+        torch.cuda.synchronize()
+        t1 = time.time()
+        words = stl.verify_batch_device(*d)
+        torch.cuda.synchronize()
+        gpu_s += time.time() - t1
+        dg.add(sig, msg, pk, stl.words_to_bool(words, n))
+        print(f"{name}: rows {c0 + n} ({time.time() - t0:.1f} s)", flush=True)
+    got = dg.result()
+    assert got["rows"] == want["rows"]
+    assert got["inputs_sha256"] == want["inputs_sha256"], "GPU signer / dataset generation differs"
+    assert got["accepted"] == want["accepted"], (got["accepted"], want["accepted"])
+    assert got["bitmap_sha256"] == want["bitmap_sha256"]
+    print(f"{name}: {got['rows']} rows, {got['accepted']} accepted, bitmap digest equal; "
+          f"verify {got['rows'] / gpu_s / 1e6:.1f} M/s incl. sync")
