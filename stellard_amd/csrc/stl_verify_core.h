@@ -372,7 +372,13 @@ STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32
   ok = ok && sc_lt_L(S) && r_is_canonical(R);  // before the decodings: R, S not live across them
   ge_p3 negA, negQ;
   bool okA, okR;
+#ifdef STL_POINT_UNPAIRED
+  // one decoding at a time (fewer live registers, more waves per SIMD)
+  okA = ge_frombytes_negate_vartime(negA, A);
+  okR = ge_frombytes_negate_vartime(negQ, R);
+#else
   ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
+#endif
   ok = ok && okA && okR;
   const bool c_neg = (o.tops & kHalfCNeg) != 0, d_neg = (o.tops & kHalfDNeg) != 0;
   const bool fits = (o.tops & kHalfFallback) == 0;
