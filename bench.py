@@ -192,11 +192,35 @@ def gpu_run(args, world, rank, local):
     n = args.n
     lo, hi = V.shard_range(n * world, rank, world)
     assert (lo, hi) == (rank * n, (rank + 1) * n) or n % 64, "per-rank shards are whole ballot words"
+    gather_via = None
+    nccl_group = None
     if world > 1:
-        # rank 0 makes the RCCL unique id; gloo carries it to every rank
-        obj = [V.comm_unique_id() if rank == 0 else None]
+        # rank 0 makes the RCCL unique id; gloo carries it to every rank.  If
+        # libstl's communicator cannot be built on some rank, every rank falls
+        # back to torch.distributed's RCCL (backend "nccl") for the gather and
+        # the line says so.
+        obj = [None]
+        if rank == 0:
+            try:
+                obj = [V.comm_unique_id()]
+            except Exception as e:  # noqa: BLE001
+                obj = [f"ERR {e!r}"]
         dist.broadcast_object_list(obj, src=0)
-        V.comm_init_rank(world, rank, obj[0])
+        err = obj[0] if isinstance(obj[0], str) else None
+        if err is None:
+            try:
+                V.comm_init_rank(world, rank, obj[0])
+            except Exception as e:  # noqa: BLE001
+                err = repr(e)
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        if any(errs):
+            if err is None:
+                V.comm_destroy()
+            nccl_group = dist.new_group(backend="nccl")
+            gather_via = "torch.distributed nccl all_gather (libstl RCCL init failed: %s)" % next(e for e in errs if e)
+        else:
+            gather_via = "libstl stl_bitmap_gather_device (ncclGather to rank 0)"
 
     # ---- synthetic data (outside the timed region) ----
     rng = np.random.default_rng(0x5EED0002 + rank)
@@ -209,10 +233,19 @@ def gpu_run(args, world, rank, local):
     full_words = torch.empty(wpr * world, dtype=torch.int64, device=dev) if world > 1 and rank == 0 else None
     stream = torch.cuda.current_stream()
 
+    def gather():
+        if nccl_group is None:
+            V.bitmap_gather_device(words, full_words, root=0, stream=stream)
+        else:
+            parts = [torch.empty_like(words) for _ in range(world)]
+            dist.all_gather(parts, words, group=nccl_group)
+            if rank == 0:
+                torch.cat(parts, out=full_words)
+
     def step():
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
         if world > 1:
-            V.bitmap_gather_device(words, full_words, root=0, stream=stream)
+            gather()
 
     for _ in range(args.warmup):
         step()
@@ -232,7 +265,7 @@ def gpu_run(args, world, rank, local):
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
         ev[k][1].record(stream)
         if world > 1:
-            V.bitmap_gather_device(words, full_words, root=0, stream=stream)
+            gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -279,8 +312,9 @@ def gpu_run(args, world, rank, local):
             "config": {"workload": "configs[1]: 1,048,576 fixed-size Payment-tx signatures per GPU "
                                    "(stl_ed25519_verify_batch_device, policy libsodium-1.0.18 + S<L)",
                        "signatures_per_gpu": n,
-                       "parallelism": f"dp{world} (index shards, libstl RCCL bitmap gather to rank 0)"
-                                      if world > 1 else "dp1"},
+                       "parallelism": f"dp{world} (index shards, RCCL bitmap gather to rank 0)"
+                                      if world > 1 else "dp1",
+                       "gather": gather_via},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
                          "kernel_ms": kern_ms, "work_per_verify": W_VERIFY,
@@ -298,7 +332,8 @@ def gpu_run(args, world, rank, local):
                 line["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)
     if world > 1:
-        V.comm_destroy()
+        if nccl_group is None:
+            V.comm_destroy()
         dist.destroy_process_group()
 
 
