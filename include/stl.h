@@ -67,6 +67,11 @@ extern "C" {
  * chain) instead of the half-size-scalar equation.
  * Same accept bits, about 1.6x slower; a cross-check / reference mode. */
 #define STL_FULL_LENGTH 0x4u
+/* Decode each distinct public key of a batch once (stellard's signers repeat:
+ * the configs-1/5 shape is 1,000 accounts for 100k transactions).  Same
+ * accept bits; costs a hash pass and extra workspace (about 100 MB per
+ * 2^20-signature chunk); does not pay when keys are all distinct. */
+#define STL_DEDUP_KEYS 0x8u
 
 /* stl_config.flags.  With two or more devices the host batch calls gather the
  * accept bitmap on device 0 with RCCL over xGMI (ncclGather / grouped
@@ -100,13 +105,12 @@ const char *stl_strerror(int rc);
  * crypto_sign_verify_detached (0 = accept, -1 = reject), plus stellard's S<L:
  * i.e. exactly RippleAddress::verifySignature's bool as 0/-1.  Runs on the GPU
  * (batch of one); returns a value < -1 on a device error.
- * LATENCY: one signature is one GPU lane; a call costs a few hundred
- * microseconds (measured), several times libsodium's
- * CPU time for a single verify, and calls serialise on the device.  Callers
- * that verify one signature at a time (stellard's JobQueue workers) should
- * submit through stl_batcher_* (throughput) or keep libsodium for the
- * latency-critical single check; this entry point is the drop-in for
- * correctness, not for speed. */
+ * LATENCY: one signature is one GPU lane, so a call is latency-bound: 643 us
+ * per call on MI355X against libsodium's 31 us, and concurrent calls
+ * serialise on the device (tools/latency.py).
+ * Callers that verify one signature at a time (stellard's JobQueue workers)
+ * keep libsodium, or submit through stl_batcher_* when many requests are in
+ * flight; this entry point is the drop-in for correctness, not for speed. */
 int stl_ed25519_verify_detached(const uint8_t *sig, const uint8_t *m, unsigned long long mlen,
                                 const uint8_t *pk);
 

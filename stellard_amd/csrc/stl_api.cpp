@@ -205,11 +205,11 @@ int ensure_init() {
 }
 
 // Workspace for (device, stream) pairs used by the device-resident API.
-int stream_workspace(Device& d, hipStream_t s, uint4** ws) {
+int stream_workspace(Device& d, hipStream_t s, uint4** ws, bool dedup = false) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
   auto& slot = d.stream_ws[s];
   if (!slot) slot.reset(new DevBuf());
-  STL_RC(slot->ensure(stl::verify_ws_bytes(d.grid)));
+  STL_RC(slot->ensure(stl::verify_ws_bytes(d.grid, dedup)));
   *ws = static_cast<uint4*>(slot->p);
   return STL_OK;
 }
@@ -338,7 +338,7 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
   STL_TRY(hipSetDevice(d.ordinal));
   STL_RC(d.bitmap.ensure(std::max<size_t>(words_alloc, 1) * 8));
   if (n == 0) return STL_OK;
-  STL_RC(d.ws.ensure(stl::verify_ws_bytes(d.grid)));
+  STL_RC(d.ws.ensure(stl::verify_ws_bytes(d.grid, (b.policy & stl::kModeDedupKeys) != 0)));
   STL_RC(d.sig.ensure(n * 64));
   STL_RC(d.msg.ensure(n * 32));
   STL_RC(d.pk.ensure(n * 32));
@@ -466,7 +466,7 @@ int gather_to_host(const Batch& b, std::vector<Shard>& sh, size_t n, size_t per,
 }
 
 int check_flags(uint32_t flags) {
-  return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH)) ? STL_EINVAL : STL_OK;
+  return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS)) ? STL_EINVAL : STL_OK;
 }
 
 int run_batch(const Batch& b, size_t n) {
@@ -753,7 +753,7 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint4* ws = nullptr;
-  STL_RC(stream_workspace(*d, s, &ws));
+  STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
                              grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s));
   return STL_OK;
@@ -769,7 +769,7 @@ int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const ui
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint4* ws = nullptr;
-  STL_RC(stream_workspace(*d, s, &ws));
+  STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_k, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
                              grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s));
   return STL_OK;

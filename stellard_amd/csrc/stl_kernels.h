@@ -16,13 +16,23 @@ constexpr size_t kWsBytesPerBlock = (size_t)kBlock * kSlotQuads * 16;
 // plus one fallback-flag word per 64 signatures
 constexpr uint32_t kPreChunk = 1u << 20;
 constexpr size_t kPreBytes = (size_t)kPreChunk * 224 + (size_t)kPreChunk / 8;
+// Per-batch key dedup (STL_DEDUP_KEYS), per kPreChunk signatures: an open-
+// addressing table of 2 * kPreChunk slots, representative / unique-id /
+// owner arrays, a counter, and the decoded keys (-A affine + ok, 5 x uint4).
+constexpr size_t kDedupSlots = 2 * (size_t)kPreChunk;
+constexpr size_t kDedupBytes = kDedupSlots * 4 + 3 * (size_t)kPreChunk * 4 + 256 + (size_t)kPreChunk * 80;
 // verify workspace for a grid of `grid` resident workgroups
-inline size_t verify_ws_bytes(uint32_t grid) { return kWsBytesPerBlock * grid + kPreBytes; }
+inline size_t verify_ws_bytes(uint32_t grid, bool dedup = false) {
+  return kWsBytesPerBlock * grid + kPreBytes + (dedup ? kDedupBytes : 0);
+}
 
 // Kernel mode word: bit 0 = policy (STL_POLICY_*), bit 8 = full-length path
-// for every lane (STL_FULL_LENGTH).
+// for every lane (STL_FULL_LENGTH), bit 9 = per-batch key dedup (STL_DEDUP_KEYS).
 constexpr uint32_t kModeFullLength = 0x100u;
-inline uint32_t kernel_mode(uint32_t flags) { return (flags & 0x1u) | ((flags & 0x4u) ? kModeFullLength : 0u); }
+constexpr uint32_t kModeDedupKeys = 0x200u;
+inline uint32_t kernel_mode(uint32_t flags) {
+  return (flags & 0x1u) | ((flags & 0x4u) ? kModeFullLength : 0u) | ((flags & 0x8u) ? kModeDedupKeys : 0u);
+}
 
 const void* kernel_verify_msg32();
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,

@@ -162,6 +162,141 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_point_k
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
 
+// ---- per-batch key dedup (STL_DEDUP_KEYS) ----
+// stellard's signers repeat (configs 1 and 5: 1,000 accounts for 100k
+// transactions), so the batch decodes each distinct key once:
+//   key_insert_kernel   open addressing on a table of 2*chunk slots: the first
+//                       lane to claim a key's slot owns it, later lanes with
+//                       the same 32 bytes point at the owner; owners get
+//                       compact ids (one atomic per wave).  At most
+//                       kKeyProbes probes: a lane that finds no slot (a
+//                       crowded or adversarial table) owns its own key, so the
+//                       work per lane stays bounded;
+//   key_decode_kernel   one lane per distinct key: the square-root chain of -A;
+//   verify_point_kernel_keyed  the point half with only R decoded.
+constexpr uint32_t kKeyEmpty = 0xffffffffu;
+constexpr int kKeyProbes = 32;
+
+__device__ __forceinline__ uint32_t key_hash(const uint32_t A[8]) {
+  uint32_t h = A[0] * 0x9E3779B1u;
+  h ^= A[1] * 0x85EBCA6Bu;
+  h = (h << 13) | (h >> 19);
+  h ^= A[2] * 0xC2B2AE35u;
+  h ^= A[5] * 0x27D4EB2Fu;
+  h ^= h >> 16;
+  return h * 0x7FEB352Du;
+}
+
+__global__ __launch_bounds__(kBlock) void key_insert_kernel(const uint8_t* __restrict__ pk, uint32_t base,
+                                                            uint32_t cnt, uint32_t* __restrict__ slots, uint32_t mask,
+                                                            uint32_t* __restrict__ rep, uint32_t* __restrict__ uid_of,
+                                                            uint32_t* __restrict__ counter,
+                                                            uint32_t* __restrict__ owners) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool live = t < cnt;
+  uint32_t r = t;
+  if (live) {
+    uint32_t A[8];
+    ld8(A, pk + 32 * ((size_t)base + t));
+    uint32_t h = key_hash(A) & mask;
+    for (int probe = 0; probe < kKeyProbes; ++probe) {
+      const uint32_t old = atomicCAS(&slots[h], kKeyEmpty, t);
+      if (old == kKeyEmpty) break;  // claimed: this lane owns the key (r == t)
+      uint32_t B[8];
+      ld8(B, pk + 32 * ((size_t)base + old));
+      bool eq = true;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) eq = eq && A[i] == B[i];
+      if (eq) {
+        r = old;
+        break;
+      }
+      h = (h + 1u) & mask;
+    }
+    rep[t] = r;
+  }
+  // compact ids for the owners: one atomic per wave
+  const bool owner = live && r == t;
+  const uint64_t m = __ballot(owner);
+  if (m == 0) return;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t b0 = 0;
+  if ((int)lane == leader) b0 = atomicAdd(counter, (uint32_t)__popcll(m));
+  b0 = __shfl(b0, leader);
+  if (owner) {
+    const uint32_t u = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    uid_of[t] = u;
+    owners[u] = t;
+  }
+}
+
+__global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __restrict__ pk, uint32_t base,
+                                                               const uint32_t* __restrict__ counter,
+                                                               const uint32_t* __restrict__ owners,
+                                                               uint4* __restrict__ keytab) {
+  const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
+  if (u >= *counter) return;  // no wave-level collective in this kernel
+  uint32_t A[8];
+  ld8(A, pk + 32 * ((size_t)base + owners[u]));
+  ge_p3 negA;
+  const bool ok = ge_frombytes_negate_vartime(negA, A);
+  uint32_t w[20];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    w[i] = negA.X.v[i];
+    w[9 + i] = negA.Y.v[i];
+  }
+  w[18] = ok ? 1u : 0u;
+  w[19] = 0;
+  uint4* q = keytab + (size_t)u * 5;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Phase 1b with the keys already decoded: only R's square-root chain, so the
+// kernel runs at more waves per SIMD than the paired one.
+__global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk, uint32_t base, uint32_t cnt, uint32_t policy,
+    uint4* __restrict__ pre, uint64_t* __restrict__ fb_words, const uint32_t* __restrict__ rep,
+    const uint32_t* __restrict__ uid_of, const uint4* __restrict__ keytab) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = t < cnt;
+  const uint32_t tt = live ? t : cnt - 1;
+  const size_t j = (size_t)base + tt;
+  uint32_t R[8], S[8], A[8];
+  ld8(R, sig + 64 * j);
+  ld8(S, sig + 64 * j + 32);
+  ld8(A, pk + 32 * j);
+  const uint4* kq = keytab + (size_t)uid_of[rep[tt]] * 5;
+  uint32_t kw[20];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint4 v = kq[i];
+    kw[4 * i] = v.x; kw[4 * i + 1] = v.y; kw[4 * i + 2] = v.z; kw[4 * i + 3] = v.w;
+  }
+  fe nAx, nAy;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    nAx.v[i] = kw[i];
+    nAy.v[i] = kw[9 + i];
+  }
+  uint4* q = pre + (size_t)tt * 14;
+  HalfState h;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&h);
+  const uint4 q2 = q[kHalfTopsWord / 4];
+  w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+  verify_phase1_points_keyed(h, R, S, A, policy & 1u, nAx, nAy, kw[18] != 0);
+  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  if (live) {
+    q[kHalfTopsWord / 4] = make_uint4(w[8], w[9], w[10], w[11]);
+#pragma unroll
+    for (int i = kHalfScalarQuads; i < 14; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  }
+  const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
+  if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
+}
+
 // Wide-table reader of the main kernel: each lane's two rows (7 x 16 B each)
 // go straight from L2 / the Infinity Cache into its wave's LDS stage by
 // global_load_lds, issued before the position's doublings -- the latency is
@@ -670,9 +805,18 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
                          const uint4* wide, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   // ws = [per-lane slots: grid x kWsBytesPerBlock][HalfState x kPreChunk][fallback words]
+  //      [dedup (kModeDedupKeys): slots, rep, uid_of, owners, counter, decoded keys]
   uint4* slots = ws;
   uint4* pre = ws + (size_t)grid * (kWsBytesPerBlock / 16);
   uint64_t* fb = reinterpret_cast<uint64_t*>(pre + (size_t)kPreChunk * 14);
+  const bool dedup = (policy & kModeDedupKeys) != 0;
+  uint32_t* dd = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws) + verify_ws_bytes(grid));
+  uint32_t* kslots = dd;
+  uint32_t* rep = kslots + kDedupSlots;
+  uint32_t* uid_of = rep + kPreChunk;
+  uint32_t* owners = uid_of + kPreChunk;
+  uint32_t* counter = owners + kPreChunk;
+  uint4* keytab = reinterpret_cast<uint4*>(counter + 64);
   for (uint64_t b64 = 0; b64 < n; b64 += kPreChunk) {  // 64-bit: n may reach 2^32 - 64
     const uint32_t base = (uint32_t)b64;
     const uint32_t cnt = n - base < kPreChunk ? n - base : kPreChunk;
@@ -683,7 +827,21 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
       hipLaunchKernelGGL(verify_scalar_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     else
       hipLaunchKernelGGL(verify_scalar_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
-    hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
+    if (dedup) {
+      uint32_t nslots = 64;
+      while (nslots < 2 * cnt) nslots <<= 1;  // <= kDedupSlots
+      hipError_t e = hipMemsetAsync(kslots, 0xff, (size_t)nslots * 4, stream);
+      if (e != hipSuccess) return e;
+      e = hipMemsetAsync(counter, 0, 4, stream);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(key_insert_kernel, g1, dim3(kBlock), 0, stream, pk, base, cnt, kslots, nslots - 1, rep, uid_of,
+                         counter, owners);
+      hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, counter, owners, keytab);
+      hipLaunchKernelGGL(verify_point_kernel_keyed, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb,
+                         rep, uid_of, keytab);
+    } else {
+      hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
+    }
     hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,

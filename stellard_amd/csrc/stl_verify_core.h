@@ -362,6 +362,20 @@ STL_HD void verify_phase1_scalars(HalfState& o, const uint32_t S[8], const uint3
   o.pad = 0;
 }
 
+// P1 = sign(c) * A, P2 = sign(d) * Q from the decoded -A, -Q; final flags.
+STL_HD void finish_phase1_points(HalfState& o, const fe& nAx, const fe& nAy, const fe& nQx, const fe& nQy, bool ok) {
+  const bool c_neg = (o.tops & kHalfCNeg) != 0, d_neg = (o.tops & kHalfDNeg) != 0;
+  const bool fits = (o.tops & kHalfFallback) == 0;
+  fe nx;
+  fe_neg(nx, nAx);
+  fe_cmov(o.P1x, nAx, nx, c_neg);
+  o.P1y = nAy;
+  fe_neg(nx, nQx);
+  fe_cmov(o.P2x, nQx, nx, d_neg);
+  o.P2y = nQy;
+  o.tops = (o.tops & 0xffu) | (ok ? kHalfOk : 0u) | (ok && !fits ? kHalfFallback : 0u);
+}
+
 // Phase 1, point half: pre-checks, decompression of A and R (the two
 // pow22523 chains, register-heavy), P1 / P2 signed by the scalar half's
 // c / d signs, final ok / fallback flags in tops.
@@ -380,16 +394,21 @@ STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32
   ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
 #endif
   ok = ok && okA && okR;
-  const bool c_neg = (o.tops & kHalfCNeg) != 0, d_neg = (o.tops & kHalfDNeg) != 0;
-  const bool fits = (o.tops & kHalfFallback) == 0;
-  fe nx;
-  fe_neg(nx, negA.X);
-  fe_cmov(o.P1x, negA.X, nx, c_neg);
-  o.P1y = negA.Y;
-  fe_neg(nx, negQ.X);
-  fe_cmov(o.P2x, negQ.X, nx, d_neg);
-  o.P2y = negQ.Y;
-  o.tops = (o.tops & 0xffu) | (ok ? kHalfOk : 0u) | (ok && !fits ? kHalfFallback : 0u);
+  finish_phase1_points(o, negA.X, negA.Y, negQ.X, negQ.Y, ok);
+}
+
+// Phase 1, point half, with -A decoded once per distinct key of the batch
+// (STL_DEDUP_KEYS: many transactions share a signer): decodes only R.  The
+// key's decoding is a function of its 32 bytes alone, so the result is the
+// same as decoding it in every lane.
+STL_HD void verify_phase1_points_keyed(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
+                                       uint32_t policy, const fe& negAx, const fe& negAy, bool okA) {
+  bool ok = verify_prechecks(R, S, A, policy);
+  ok = ok && sc_lt_L(S) && r_is_canonical(R);
+  ge_p3 negQ;
+  const bool okR = ge_frombytes_negate_vartime(negQ, R);
+  ok = ok && okA && okR;
+  finish_phase1_points(o, negAx, negAy, negQ.X, negQ.Y, ok);
 }
 
 STL_HD void verify_phase1_half(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],

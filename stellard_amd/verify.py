@@ -23,6 +23,8 @@ POLICY_SODIUM_1_0_18 = N.STL_POLICY_SODIUM_1_0_18
 POLICY_STELLARD_1_0_0 = N.STL_POLICY_STELLARD_1_0_0
 # OR into `policy` to check with full-length scalars (same bits, slower)
 FULL_LENGTH = N.STL_FULL_LENGTH
+# OR into `policy` to decode each distinct public key of a batch once
+DEDUP_KEYS = N.STL_DEDUP_KEYS
 
 
 class BadInputs(RuntimeError):

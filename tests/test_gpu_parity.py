@@ -466,3 +466,37 @@ def test_batcher_verdicts(stl, oracle, golden):
         assert np.array_equal(gt, want)
         s = b.stats()
         assert s["completed"] == len(sig) + len(blobs)
+
+
+@pytest.mark.parametrize("policy", [0, 1, 4])
+def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
+    """STL_DEDUP_KEYS (each distinct key decoded once per batch) gives the same
+    bits as the default path: golden rows (every adversarial key class, keys
+    repeated across rows), and a 1,000-signer batch with mutations that
+    straddles the 2^20-signature chunk, on the host and device entry points."""
+    torch = torch_cuda
+    sig, msg, pk = golden["sig"], golden["msg"], golden["pk"]
+    key = "expected_stellard_1_0_0_unpinned" if policy & 1 else "expected_sodium_1_0_18"
+    idx = np.random.default_rng(3).integers(0, sig.shape[0], 20000)
+    got = stl.verify_batch(sig[idx], msg[idx], pk[idx], policy=policy | stl.DEDUP_KEYS)
+    assert np.array_equal(got, golden[key][idx].astype(bool))
+    # 1,000 signers, (1 << 20) + 4099 rows: two chunks, keys shared across both
+    n = (1 << 20) + 4099
+    rng = np.random.default_rng(5)
+    aseed = rng.integers(0, 256, (1000, 32), dtype=np.uint8)
+    who = rng.integers(0, 1000, n)
+    seeds = torch.from_numpy(aseed[who]).cuda()
+    msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    pkd, sigd = stl.sign_batch_device(seeds, msgs)
+    s_np, m_np, p_np = sigd.cpu().numpy(), msgs.cpu().numpy(), pkd.cpu().numpy()
+    bad = rng.random(n) < 0.05
+    s_np[bad, 40] ^= 0x20
+    d = [torch.from_numpy(a).cuda() for a in (s_np, m_np, p_np)]
+    w0 = stl.verify_batch_device(*d, policy=policy)
+    w1 = stl.verify_batch_device(*d, policy=policy | stl.DEDUP_KEYS)
+    torch.cuda.synchronize()
+    b0, b1 = stl.words_to_bool(w0, n), stl.words_to_bool(w1, n)
+    assert np.array_equal(b0, b1)
+    assert np.array_equal(b1, ~bad)
+    samp = rng.choice(n, 4000, replace=False)
+    assert np.array_equal(b1[samp], oracle.verify_batch(s_np[samp], m_np[samp], p_np[samp], policy=policy & 1))
