@@ -104,15 +104,15 @@ class Gpu:
         pk, sig = self.V.sign_batch_device(t.from_numpy(seeds).cuda(), t.from_numpy(msgs).cuda())
         return pk, sig
 
-    def verify_dev(self, sig, msg, pk, reps=5):
+    def verify_dev(self, sig, msg, pk, reps=5, policy=0):
         t = self.torch
-        words = self.V.verify_batch_device(sig, msg, pk, stream=self.stream)
+        words = self.V.verify_batch_device(sig, msg, pk, stream=self.stream, policy=policy)
         t.cuda.synchronize()
         times = []
         for _ in range(reps):
             a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
             a.record(self.stream)
-            self.V.verify_batch_device(sig, msg, pk, out_words=words, stream=self.stream)
+            self.V.verify_batch_device(sig, msg, pk, out_words=words, stream=self.stream, policy=policy)
             b.record(self.stream)
             t.cuda.synchronize()
             times.append(a.elapsed_time(b) * 1e-3)
@@ -225,6 +225,18 @@ def tx_config(gpu, cpu, n, rng, pad_lens, cpu_samples):
         times.append(a.elapsed_time(b) * 1e-3)
     dev_bits = gpu.V.words_to_bool(words, n)
     dev_s = float(np.median(times[1:]))
+    # the same with STL_DEDUP_KEYS (1,000 signers: each key decoded once per batch)
+    times = []
+    for _ in range(6):
+        a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+        a.record(gpu.stream)
+        gpu.tx_hash_dev(d_blob, d_off, d_len, n, d_msg)
+        gpu.V.verify_batch_device(sig, d_msg, pk, out_words=words, stream=gpu.stream, policy=gpu.V.DEDUP_KEYS)
+        b.record(gpu.stream)
+        t.cuda.synchronize()
+        times.append(a.elapsed_time(b) * 1e-3)
+    dedup_bits = gpu.V.words_to_bool(words, n)
+    dedup_s = float(np.median(times[1:]))
     # host API (PCIe-inclusive): one stl_tx_verify_batch call on packed host buffers
     bm = np.zeros((n + 7) // 8, np.uint8)
     B = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
@@ -245,9 +257,11 @@ def tx_config(gpu, cpu, n, rng, pad_lens, cpu_samples):
         "n": n, "preimage_bytes": {"min": int(lens.min()), "median": int(np.median(lens)), "max": int(lens.max()),
                                    "total": int(lens.sum())},
         "gpu_device_resident_tx_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
+        "gpu_device_resident_dedup_keys_tx_per_s": n / dedup_s, "gpu_device_dedup_keys_ms": dedup_s * 1e3,
         "gpu_host_api_tx_per_s": n / host_s,
         "cpu_reference": cpu_rates(run, n, cpu_samples),
         "bitmap_parity": {"rows": n, "mismatches_device": int((dev_bits != ref_bits).sum()),
+                          "mismatches_device_dedup_keys": int((dedup_bits != ref_bits).sum()),
                           "mismatches_host_api": int((host_bits != ref_bits).sum()),
                           "accepted": int(ref_bits.sum())},
         "cpu_full_run_16_threads_s": ref_s,
@@ -331,6 +345,7 @@ def config2(gpu, cpu):
     pk, sig = gpu.sign(seeds, msgs)
     d_msg = t.from_numpy(msgs).cuda()
     bits, dev_s = gpu.verify_dev(sig, d_msg, pk)
+    dbits, dedup_s = gpu.verify_dev(sig, d_msg, pk, policy=gpu.V.DEDUP_KEYS)  # all keys distinct: overhead only
     s_np, p_np = sig.cpu().numpy(), pk.cpu().numpy()
     hb, host_s = timed(lambda: gpu.V.verify_batch(s_np, msgs, p_np))
     hb, host_s = timed(lambda: gpu.V.verify_batch(s_np, msgs, p_np))
@@ -341,6 +356,7 @@ def config2(gpu, cpu):
     sample = 1 << 18
     ref = run(0, sample, 16)
     return {"n": n, "gpu_device_resident_verifies_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
+            "gpu_device_dedup_keys_ms_all_distinct": dedup_s * 1e3, "dedup_bits_equal": bool((dbits == bits).all()),
             "gpu_host_api_verifies_per_s": n / host_s,
             "cpu_reference": cpu_rates(run, n, [(16, 1 << 19), (6, 1 << 18), (1, 1 << 15)]),
             "bitmap_parity": {"rows": sample, "mismatches": int((bits[:sample] != ref).sum()),
