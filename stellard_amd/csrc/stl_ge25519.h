@@ -51,6 +51,9 @@ STL_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
 }
 
 // dbl-2008-hwcd (a = -1): p2 [1] -> p1p1 with X,T [1], Y [2], Z [3].
+// TO_P2: the result only feeds ge_p1p1_to_p2 (X*T, Y*Z, Z*T; no X*Y), so X
+// may stay lazy: X = A + 3*Z1 - Y [<= 4] (Y [<= 2+2^-11] < 3), X*T <= 4.
+template <bool TO_P2 = false>
 STL_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe XX, YY, ZZ2, A, XpY;
   fe_add(XpY, p.X, p.Y);     // [2]
@@ -58,7 +61,10 @@ STL_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe_add(ZZ2, ZZ2, ZZ2);     // [2]
   fe_add(r.Y, YY, XX);       // [2]
   fe_sub_nc<2>(r.Z, YY, XX); // [3]
-  fe_sub(r.X, A, r.Y);       // [1]
+  if (TO_P2)
+    fe_sub_nc<3>(r.X, A, r.Y);  // [4]
+  else
+    fe_sub(r.X, A, r.Y);     // [1]
   fe_sub(r.T, ZZ2, r.Z);     // [1]
 }
 

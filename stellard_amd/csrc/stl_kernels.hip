@@ -31,7 +31,11 @@
 #define STL_VERIFY_WAVES_PER_SIMD 2
 #endif
 #ifndef STL_PRE_WAVES_PER_SIMD
+#ifdef STL_POINT_PAIRED
 #define STL_PRE_WAVES_PER_SIMD 2
+#else
+#define STL_PRE_WAVES_PER_SIMD 4
+#endif
 #endif
 // Scalar half of phase 1 (SHA-512 of k, lattice reduction): serial
 // dependency chains with few live registers, so occupancy hides latency.
