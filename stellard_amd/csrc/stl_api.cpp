@@ -267,7 +267,10 @@ void shard_bytes_bounds(const uint32_t* len, size_t n, int g, std::vector<size_t
 // (preimages, blobs) are copied up to a watermark: chunk c copies
 // [watermark, max end of its rows), rebased on the shard's lowest offset, so
 // any offset order is correct.
-constexpr size_t kPipeChunk = (size_t)1 << 18;
+#ifndef STL_PIPE_CHUNK_LOG2
+#define STL_PIPE_CHUNK_LOG2 17  // 128K: one full round of resident main-kernel waves; A/B in DESIGN.md section 8
+#endif
+constexpr size_t kPipeChunk = (size_t)1 << STL_PIPE_CHUNK_LOG2;
 
 enum class Mode { kSig, kPre, kBlob };
 
