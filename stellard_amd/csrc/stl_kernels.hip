@@ -342,17 +342,55 @@ struct WideLds {
   }
 };
 
+// Experiment switch (STL_WIDE_GLOBAL): rows read straight into VGPRs at the
+// madd, no LDS stage (the stage's 57 KB per workgroup caps the kernel at two
+// workgroups = 2 waves/SIMD per CU).
+struct WideGlobal {
+  const uint4* gtab;
+  int d[2];
+  __device__ void prefetch(int d0, int d1) {
+    d[0] = d0;
+    d[1] = d1;
+  }
+  __device__ void madd(ge_p1p1& t, const ge_p3& acc, int which) const {
+    const uint32_t a = (uint32_t)(d[which] < 0 ? -d[which] : d[which]);
+    const uint4* src = gtab + ((size_t)which * kWideEntries + a) * 7;
+    ge_niels n;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&n);
+    uint32_t row[28];
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+      const uint4 v = src[c];
+      row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 27; ++i) w[i] = row[i];
+    ge_niels_cneg(n, d[which] < 0);
+    ge_madd(t, acc, n);
+  }
+};
+
 // Phase 2: [e]B + [c](-A) + [d](-Q) == O; grid-strides over 256-signature
 // tiles of [base, base+cnt) so the per-lane table workspace is bounded by the
 // resident lanes; one ballot word per wave.
-__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_kernel(
+#ifdef STL_MAIN_NUM_VGPR
+#define STL_MAIN_ATTR __attribute__((amdgpu_num_vgpr(STL_MAIN_NUM_VGPR)))
+#else
+#define STL_MAIN_ATTR
+#endif
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
     uint4* __restrict__ ws, const uint4* __restrict__ wide) {
-  __shared__ uint4 wstage[kBlock / 64][2 * 7 * 64];
   uint4* slot = lane_slot(ws);
   const TableView tab1{slot, 1}, tab2{slot + kTableQuads, 1};
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+#ifdef STL_WIDE_GLOBAL
+  WideGlobal wl{wide, {0, 0}};
+  (void)lane;
+#else
+  __shared__ uint4 wstage[kBlock / 64][2 * 7 * 64];
   WideLds wl{wide, wstage[wave], lane, {0, 0}};
+#endif
   for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
     const uint32_t t = tile + threadIdx.x;
     const bool live = t < cnt;

@@ -583,10 +583,16 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     // of independent work per wave): their latency (L2 / Infinity Cache) is
     // hidden instead of stalling the adds.
     ge_cached ca, cq;
+#ifndef STL_NO_TABLE_PREFETCH
     tab1.load(dc < 0 ? -dc : dc, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
+#endif
     if (bpos) wide.prefetch(de0, de1);
     if (i != npos - 1) dbl4(acc, acc2);
+#ifdef STL_NO_TABLE_PREFETCH
+    tab1.load(dc < 0 ? -dc : dc, ca);
+    tab2.load(dq < 0 ? -dq : dq, cq);
+#endif
     ge_cached_cneg(ca, dc < 0);
     ge_add_cached(t, acc, ca);
     ge_p1p1_to_p3(acc, t);
