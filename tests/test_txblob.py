@@ -145,3 +145,71 @@ def test_blob_words_unaligned(emu, off):
         out = (ctypes.c_uint32 * n)()
         emu.hostemu_blob_words(buf.ctypes.data_as(ctypes.c_void_p), off, n, ln, out)
         assert bytes(np.array(out, np.uint32).tobytes()) == buf[off:off + 4 * n].tobytes()
+
+
+# ---- serialized validations -------------------------------
+VALIDATION = 1
+
+
+@pytest.fixture(scope="module")
+def val_corpus(oracle):
+    rng = np.random.default_rng(77)
+    keys = [oracle.keypair(rng.bytes(32)) for _ in range(4)]
+    out = []
+    for i in range(160):
+        pk, sk = keys[i % 4]
+        fs = T.validation_fields(rng, pk, full=bool(i % 3))
+        blob, h, _ = T.signed_validation(fs, sk, oracle.sign)
+        out.append((blob, T.validation_preimage(fs), h))
+    return out
+
+
+def test_oracle_reserialises_validations(oracle, val_corpus):
+    """SerializedValidation(sit) + getSigningHash (SerializedValidation.cpp:22-34,
+    70-73): the C re-serialiser gives back the Python blob and "VAL\\0" ||
+    fields without Signature; libsodium accepts the signatures over it."""
+    from tests.oracle_bind import sodium_signed_blob_verify_batch
+    for blob, pre, h in val_corpus:
+        ok, info, signing, full = oracle.signed_blob(VALIDATION, blob)
+        assert ok and full == blob and signing == pre
+        assert h512half(signing) == h
+        assert info.pk_len == 32 and info.sig_len == 64
+    blobs = [b for b, _, _ in val_corpus]
+    bits, ids = oracle.signed_blob_verify_batch(VALIDATION, blobs, ids=True)
+    assert bits.all()
+    assert all(bytes(i) == h512half(b) for i, b in zip(ids, blobs))  # PeerImp.cpp:1155 suppression key
+    ref = load_sodium_ref()
+    if ref is not None:
+        assert sodium_signed_blob_verify_batch(ref, VALIDATION, blobs).all()
+    # as transactions they do not verify (no TransactionType, no TxnSignature)
+    assert not oracle.tx_blob_verify_batch(blobs).any()
+
+
+def test_device_pass_on_validations_and_fuzz(oracle, emu, val_corpus):
+    """The device pass for validations (BlobKind: "VAL\\0", sfSignature, id =
+    SHA512Half(raw), 50-byte floor) against the oracle on the corpus and on
+    3,000 mutated blobs: wherever the device decides, the reference
+    re-serialises unchanged and the signing hash / id / status agree."""
+    from tests.oracle_bind import hostemu_signed_blob
+    blobs = [b for b, _, _ in val_corpus]
+    for blob, pre, h in val_corpus:
+        st, msg, idb = hostemu_signed_blob(emu, VALIDATION, blob)
+        assert st == OK and msg == h and idb == h512half(blob)
+    rng = np.random.default_rng(78)
+    counts = {OK: 0, DEFERRED: 0, MALFORMED: 0}
+    for _ in range(3000):
+        m = T.mutate(rng, blobs[int(rng.integers(len(blobs)))])
+        st, msg, idb = hostemu_signed_blob(emu, VALIDATION, m)
+        counts[st] += 1
+        ok, info, signing, full = oracle.signed_blob(VALIDATION, m)
+        if st == DEFERRED or not ok:
+            continue
+        assert full == m and not info.stopped_early, m.hex()
+        assert idb == h512half(m)
+        assert st == (OK if (info.pk_len == 32 and info.sig_len == 64) else MALFORMED)
+        if st == OK:
+            assert msg == h512half(signing)
+    assert counts[OK] > 100 and counts[DEFERRED] > 100, counts
+    # below PeerImp::recvValidation's 50-byte floor: deferred
+    short = blobs[0][:49]
+    assert hostemu_signed_blob(emu, VALIDATION, short)[0] == DEFERRED
