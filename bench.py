@@ -256,6 +256,7 @@ def gpu_run(args, world, rank, local):
 
     # ---- timed region: exactly K steps between barrier+sync on both sides ----
     torch.cuda.synchronize()
+    V.reset_stats()
     if world > 1:
         dist.barrier()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -278,6 +279,7 @@ def gpu_run(args, world, rank, local):
     if world > 1 and rank == 0:
         assert V.words_to_bool(full_words, n * world).all(), "gathered bitmap has rejects"
 
+    st = V.get_stats()  # device counters over the K timed launches (after the sync above)
     if rank == 0:
         total = n * world * args.steps
         value = total / dt
@@ -323,6 +325,9 @@ def gpu_run(args, world, rank, local):
                          "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9),
                          "valu_busy_pmc": valu_busy},
             "cpu_baseline": None,
+            "stats": {"source": "stl_get_stats over the timed launches (rank 0)",
+                      "accepted": st["accepted"], "full_length_lanes": st["full_length_lanes"],
+                      "verifies": n * args.steps},
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -252,6 +252,24 @@ void stl_batcher_stats(stl_batcher *b, uint64_t *submitted, uint64_t *completed,
 /* Completes every pending request, then frees the aggregator. */
 void stl_batcher_destroy(stl_batcher *b);
 
+/* ---- statistics and tracing (metrics) ----
+ * Cumulative since stl_init / stl_reset_stats.  Host side: entry-point calls
+ * (the host batch / tx / blob calls), signatures submitted, calls that
+ * returned < 0, wall time inside them and in the multi-GPU gather.  Device
+ * side (every verify launch, host and device entry points): accept bits
+ * written and signatures checked by the full-length fallback path.  Reading
+ * the device counters synchronises the devices.  STL_TRACE=1 in the
+ * environment at stl_init prints one JSON line per host call on stderr. */
+typedef struct stl_stats {
+  uint32_t struct_size; /* sizeof(stl_stats) */
+  uint32_t reserved;
+  uint64_t batches, signatures, errors;
+  uint64_t host_ns, gather_ns;
+  uint64_t accepted, full_length_lanes;
+} stl_stats;
+int stl_get_stats(stl_stats *out);
+void stl_reset_stats(void);
+
 /* ---- testing hooks ----
  * Fault injection: after `calls` further HIP/RCCL calls made by libstl the
  * next one reports failure without running (one shot); calls < 0 disarms.

@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -137,6 +139,7 @@ struct Device {
   ncclComm_t comm = nullptr;     // in-process communicator (rank = device index)
   std::mutex mu;
   DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide, gather;
+  DevBuf counters;  // device u64 counters of stl_get_stats: [0] accepted, [1] full-length lanes
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;  // tx-hash work counter
   std::mutex ws_mu;
@@ -152,6 +155,39 @@ bool g_comm_gather = false;  // host batches gather their bitmap over RCCL
 std::mutex g_pcomm_mu;
 ncclComm_t g_pcomm = nullptr;
 int g_pcomm_ranks = 0;
+
+unsigned long long* dev_counters(Device& d) { return static_cast<unsigned long long*>(d.counters.p); }
+
+// ---- host-side statistics (stl_get_stats) and tracing (STL_TRACE=1) ----
+std::atomic<uint64_t> g_st_batches{0}, g_st_sigs{0}, g_st_errors{0}, g_st_host_ns{0}, g_st_gather_ns{0};
+bool g_trace = false;
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// Counts one host entry-point call: signatures, wall time, errors; with
+// STL_TRACE=1 one JSON line per call on stderr (host spans; the kernels are
+// rocprofv3's).
+struct CallSpan {
+  const char* name;
+  size_t n;
+  uint64_t t0 = now_ns();
+  int finish(int rc, uint64_t gather_ns = 0) {
+    const uint64_t dt = now_ns() - t0;
+    g_st_batches++;
+    g_st_sigs += n;
+    g_st_host_ns += dt;
+    g_st_gather_ns += gather_ns;
+    if (rc < 0) g_st_errors++;
+    if (g_trace)
+      std::fprintf(stderr, "{\"stl_trace\": \"%s\", \"n\": %zu, \"rc\": %d, \"ms\": %.3f, \"gather_ms\": %.3f}\n", name, n,
+                   rc, dt * 1e-6, gather_ns * 1e-6);
+    return rc;
+  }
+};
 
 int current_device_index() {
   int ord = -1;
@@ -173,6 +209,8 @@ int setup_device(Device& d) {
   d.grid = (uint32_t)(d.cus * per_cu);
   STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   STL_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  STL_RC(d.counters.ensure(64));
+  STL_TRY(hipMemsetAsync(d.counters.p, 0, 64, d.stream));
   // wide base tables for [e]B (7.3 MB), built once on the device
   STL_RC(d.wide.ensure(stl::kWideTableBytes));
   STL_TRY(stl::launch_wide_table(static_cast<uint4*>(d.wide.p), d.stream));
@@ -187,7 +225,7 @@ void release_device(Device& d) {
   if (d.comm && g_rccl.ok) (void)g_rccl.CommDestroy(d.comm);
   d.comm = nullptr;
   for (DevBuf* b : {&d.ws, &d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.txid, &d.status,
-                    &d.wide, &d.gather})
+                    &d.wide, &d.gather, &d.counters})
     b->release();
   for (auto& kv : d.stream_ws) kv.second->release();
   for (auto& kv : d.stream_ctr) kv.second->release();
@@ -390,7 +428,8 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
                                   static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream, b.kind));
     STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
                                static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, static_cast<uint4*>(d.ws.p),
-                               grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream));
+                               grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream,
+                               dev_counters(d)));
   }
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
   if (dtxid) STL_TRY(hipMemcpyAsync(b.txid + 32 * lo, dtxid, n * 32, hipMemcpyDeviceToHost, d.stream));
@@ -472,7 +511,7 @@ int check_flags(uint32_t flags) {
   return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS)) ? STL_EINVAL : STL_OK;
 }
 
-int run_batch(const Batch& b, size_t n) {
+int run_batch(const Batch& b, size_t n, uint64_t* gather_ns) {
   if (n == 0) return STL_OK;
   STL_RC(ensure_init());
   const int g = (int)g_devs.size();
@@ -508,7 +547,11 @@ int run_batch(const Batch& b, size_t n) {
     for (auto& t : th) t.join();
     int rc = STL_OK;
     for (auto& s : sh) rc = rc ? rc : s.rc;
-    if (rc == STL_OK) rc = gather_to_host(b, sh, n, per, !by_bytes);
+    if (rc == STL_OK) {
+      const uint64_t g0 = now_ns();
+      rc = gather_to_host(b, sh, n, per, !by_bytes);
+      *gather_ns = now_ns() - g0;
+    }
     for (auto& d : g_devs) {
       const int drc = drain(*d);
       rc = rc ? rc : drc;
@@ -540,6 +583,7 @@ int stl_init(const stl_config* cfg) {
   if (g_init) return STL_OK;
   const char* fa = std::getenv("STL_FAULT_AFTER");
   if (fa && *fa) g_fault_after.store(std::atoll(fa));
+  g_trace = env_int("STL_TRACE", 0) != 0;
   int first = 0, want = -1, spd = 1;
   uint32_t cflags = 0;
   if (cfg) {  // argument checks first: they need no device
@@ -632,6 +676,39 @@ const char* stl_strerror(int rc) {
 
 void stl_debug_fault_after(long long calls) { g_fault_after.store(calls < 0 ? -1 : calls); }
 
+int stl_get_stats(stl_stats* out) {
+  if (!out || out->struct_size != sizeof(stl_stats)) return STL_EINVAL;
+  out->batches = g_st_batches.load();
+  out->signatures = g_st_sigs.load();
+  out->errors = g_st_errors.load();
+  out->host_ns = g_st_host_ns.load();
+  out->gather_ns = g_st_gather_ns.load();
+  out->accepted = 0;
+  out->full_length_lanes = 0;
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& d : g_devs) {  // device counters: waits for the work queued before the call
+    if (!d->counters.p) continue;
+    unsigned long long c[2] = {0, 0};
+    if (hipSetDevice(d->ordinal) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(c, d->counters.p, sizeof c, hipMemcpyDeviceToHost) != hipSuccess)
+      return STL_EHIP;
+    out->accepted += c[0];
+    out->full_length_lanes += c[1];
+  }
+  return STL_OK;
+}
+
+void stl_reset_stats(void) {
+  g_st_batches = 0;
+  g_st_sigs = 0;
+  g_st_errors = 0;
+  g_st_host_ns = 0;
+  g_st_gather_ns = 0;
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& d : g_devs)
+    if (d->counters.p && hipSetDevice(d->ordinal) == hipSuccess) (void)hipMemset(d->counters.p, 0, 64);
+}
+
 void stl_shard_range(size_t n, int r, int g, size_t* lo, size_t* hi) {
   if (!lo || !hi) return;
   if (g < 1 || r < 0 || r >= g) {
@@ -660,7 +737,10 @@ int stl_ed25519_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8
   STL_RC(check_flags(flags));
   const Batch b{Mode::kSig, sig, msg, pk, nullptr, nullptr, nullptr, accept_bitmap, nullptr, nullptr,
                 stl::kernel_mode(flags), 0u};
-  return run_batch(b, n);
+  CallSpan span{"stl_ed25519_verify_batch", n};
+  uint64_t g = 0;
+  const int rc = run_batch(b, n, &g);
+  return span.finish(rc, g);
 }
 
 int stl_tx_verify_batch(const uint8_t* preimages, const uint64_t* offset, const uint32_t* len, const uint8_t* sig,
@@ -670,7 +750,10 @@ int stl_tx_verify_batch(const uint8_t* preimages, const uint64_t* offset, const 
   STL_RC(check_flags(flags));
   const Batch b{Mode::kPre, sig, nullptr, pk, preimages, offset, len, accept_bitmap, nullptr, nullptr,
                 stl::kernel_mode(flags), 0u};
-  return run_batch(b, n);
+  CallSpan span{"stl_tx_verify_batch", n};
+  uint64_t g = 0;
+  const int rc = run_batch(b, n, &g);
+  return span.finish(rc, g);
 }
 
 int stl_signed_blob_verify_batch(uint32_t kind, const uint8_t* blobs, const uint64_t* offset, const uint32_t* len,
@@ -681,7 +764,11 @@ int stl_signed_blob_verify_batch(uint32_t kind, const uint8_t* blobs, const uint
   STL_RC(check_flags(flags));
   const Batch b{Mode::kBlob, nullptr, nullptr, nullptr, blobs, offset, len, accept_bitmap, status, id,
                 stl::kernel_mode(flags), kind};
-  return run_batch(b, n);
+  CallSpan span{kind == STL_BLOB_VALIDATION ? "stl_signed_blob_verify_batch(validation)" : "stl_tx_blob_verify_batch",
+                n};
+  uint64_t g = 0;
+  const int rc = run_batch(b, n, &g);
+  return span.finish(rc, g);
 }
 
 int stl_tx_blob_verify_batch(const uint8_t* blobs, const uint64_t* offset, const uint32_t* len, size_t n,
@@ -725,7 +812,7 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
     STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                                static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
                                STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true,
-                               static_cast<const uint4*>(d.wide.p), s));
+                               static_cast<const uint4*>(d.wide.p), s, dev_counters(d)));
     STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
     STL_TRY(hipStreamSynchronize(s));
     return STL_OK;
@@ -758,7 +845,7 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   uint4* ws = nullptr;
   STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s));
+                             grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d)));
   return STL_OK;
 }
 
@@ -774,7 +861,7 @@ int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const ui
   uint4* ws = nullptr;
   STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_k, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s));
+                             grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d)));
   return STL_OK;
 }
 

@@ -380,7 +380,7 @@ struct WideGlobal {
 #endif
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
-    uint4* __restrict__ ws, const uint4* __restrict__ wide) {
+    uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr) {
   uint4* slot = lane_slot(ws);
   const TableView tab1{slot, 1}, tab2{slot + kTableQuads, 1};
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -399,7 +399,10 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const bool ok = verify_phase2_half(h, tab1, tab2, wl) && live;
     const uint64_t word = __ballot(ok);
     const uint32_t wbase = tile + wave * 64;
-    if (lane == 0 && wbase < cnt) bitmap[(base + wbase) >> 6] = word;
+    if (lane == 0 && wbase < cnt) {
+      bitmap[(base + wbase) >> 6] = word;
+      if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popcll(word));  // accepted (stl_get_stats)
+    }
   }
 }
 
@@ -410,7 +413,7 @@ template <bool PRE_K>
 __global__ __launch_bounds__(kBlock, 2) void verify_fallback_kernel(
     const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
     uint32_t base, uint32_t cnt, uint32_t policy, const uint64_t* __restrict__ fb_words,
-    uint64_t* __restrict__ bitmap, uint4* __restrict__ ws) {
+    uint64_t* __restrict__ bitmap, uint4* __restrict__ ws, unsigned long long* __restrict__ ctr) {
   __shared__ uint32_t sB[kBaseTableWords];
   stage_base_table(sB, 1);
   const TableView tab{lane_slot(ws), 1};
@@ -431,7 +434,13 @@ __global__ __launch_bounds__(kBlock, 2) void verify_fallback_kernel(
       ok = verify_full_with_k(R, S, A, k, policy & 1u, tab, sB);
     }
     const uint64_t word = __ballot(ok);
-    if (lane == 0) bitmap[(base + wbase) >> 6] |= word;
+    if (lane == 0) {
+      bitmap[(base + wbase) >> 6] |= word;
+      if (ctr) {  // full-length lanes and their accepts (stl_get_stats)
+        atomicAdd(&ctr[1], (unsigned long long)__popcll(fb));
+        atomicAdd(&ctr[0], (unsigned long long)__popcll(word));
+      }
+    }
   }
 }
 
@@ -844,7 +853,7 @@ hipError_t launch_wide_table(uint4* out, hipStream_t stream) {
 
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
-                         const uint4* wide, hipStream_t stream) {
+                         const uint4* wide, hipStream_t stream, unsigned long long* counters) {
   if (n == 0) return hipSuccess;
   // ws = [per-lane slots: grid x kWsBytesPerBlock][HalfState x kPreChunk][fallback words]
   //      [dedup (kModeDedupKeys): slots, rep, uid_of, owners, counter, decoded keys]
@@ -884,13 +893,14 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     } else {
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
-    hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide);
+    hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
+                       counters);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                         policy, fb, bitmap, slots);
+                         policy, fb, bitmap, slots, counters);
     else
       hipLaunchKernelGGL(verify_fallback_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                         policy, fb, bitmap, slots);
+                         policy, fb, bitmap, slots, counters);
   }
   return hipGetLastError();
 }

@@ -414,6 +414,26 @@ def bitmap_gather_device(words, out_words=None, root=0, stream=None):
     return out_words
 
 
+# ---- statistics (include/stl.h stl_get_stats) ----
+
+class Stats(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("batches", ctypes.c_uint64), ("signatures", ctypes.c_uint64), ("errors", ctypes.c_uint64),
+                ("host_ns", ctypes.c_uint64), ("gather_ns", ctypes.c_uint64),
+                ("accepted", ctypes.c_uint64), ("full_length_lanes", ctypes.c_uint64)]
+
+
+def get_stats():
+    st = Stats()
+    st.struct_size = ctypes.sizeof(Stats)
+    N.check(N.load().stl_get_stats(ctypes.byref(st)), "stl_get_stats")
+    return {name: getattr(st, name) for name, _ in Stats._fields_ if name not in ("struct_size", "reserved")}
+
+
+def reset_stats():
+    N.load().stl_reset_stats()
+
+
 # ---- testing hooks ----
 
 def debug_fault_after(calls):

@@ -131,10 +131,16 @@ def test_mixed_fallback_lanes_in_one_wave(stl, torch_cuda, oracle):
     assert all(flagged[w * 64:(w + 1) * 64].any() and (~flagged[w * 64:(w + 1) * 64]).any() for w in range(4))
     d = [torch.from_numpy(np.frombuffer(b"".join(x), np.uint8).reshape(n, -1).copy()).cuda() for x in (sig, kk, pk)]
     for flags in (0, stl.FULL_LENGTH):
+        stl.reset_stats()
         words = stl.debug_verify_k_device(d[0], d[1], d[2], policy=flags)
         torch.cuda.synchronize()
         got = stl.words_to_bool(words, n)
         assert np.array_equal(got, exp), (flags, np.nonzero(got != exp)[0][:10])
+        # device counters (stl_get_stats): the accepts, and exactly the
+        # contrived lanes through the full-length path (every lane with the flag)
+        st = stl.get_stats()
+        assert st["accepted"] == int(exp.sum())
+        assert st["full_length_lanes"] == (n if flags else int(flagged.sum())), st
 
 
 # ------------------------------------------------------- multi-shard / RCCL
@@ -279,6 +285,25 @@ def test_fault_injection_every_entry_point(stl, torch_cuda, oracle, golden, mode
                 pytest.fail(f"{name}: still failing after 80 injected faults")
             report[name] = hits
         assert all(h >= 1 for h in report.values()), report
+
+
+def test_stats_count_calls_signatures_and_errors(stl, golden):
+    """stl_get_stats (SURVEY.md section 5 metrics): host calls, signatures,
+    errors, device accepts."""
+    sig, msg, pk, exp = _golden_rows(golden, 5000, seed=8)
+    stl.reset_stats()
+    got = stl.verify_batch(sig, msg, pk)
+    assert np.array_equal(got, exp)
+    st = stl.get_stats()
+    assert st["batches"] == 1 and st["signatures"] == 5000 and st["errors"] == 0
+    assert st["accepted"] == int(exp.sum()) and st["host_ns"] > 0
+    stl.debug_fault_after(0)
+    from stellard_amd import _native as N
+    with pytest.raises(N.StlError):
+        stl.verify_batch(sig, msg, pk)
+    stl.debug_fault_after(-1)
+    st = stl.get_stats()
+    assert st["batches"] == 2 and st["errors"] == 1
 
 
 def test_fault_injection_batcher_delivers_errors(stl, oracle, golden):

@@ -200,3 +200,23 @@ def test_batcher_flush_with_nothing_pending_keeps_the_delay():
         waited = time.perf_counter() - t0
         assert v < 0
         assert waited >= 0.3, waited
+
+
+def test_stats_without_gpu():
+    """stl_get_stats on a GPU-less host: host counters only; a failed call is
+    counted as an error (ENODEV), nothing as verified-and-accepted."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    from stellard_amd import _native as N
+    from stellard_amd import verify as V
+    V.reset_stats()
+    sig = np.zeros((64, 64), np.uint8)
+    msg = np.zeros((64, 32), np.uint8)
+    with pytest.raises(N.StlError):
+        V.verify_batch(sig, msg, msg)
+    st = V.get_stats()
+    assert st["batches"] == 1 and st["signatures"] == 64 and st["errors"] == 1 and st["accepted"] == 0
+    bad = V.Stats()
+    bad.struct_size = 8
+    assert N.load().stl_get_stats(ctypes.byref(bad)) == N.STL_EINVAL
