@@ -20,7 +20,11 @@ constexpr size_t kPreBytes = (size_t)kPreChunk * 224 + (size_t)kPreChunk / 8;
 // addressing table of 2 * kPreChunk slots, representative / unique-id /
 // owner arrays, a counter, and the decoded keys (-A affine + ok, 5 x uint4).
 constexpr size_t kDedupSlots = 2 * (size_t)kPreChunk;
-constexpr size_t kDedupBytes = kDedupSlots * 4 + 3 * (size_t)kPreChunk * 4 + 256 + (size_t)kPreChunk * 80;
+// shared per-key A-tables (9 cached entries, 1,296 B) for up to kKeyTables
+// distinct keys per chunk; above that the chunk builds per-lane tables
+constexpr uint32_t kKeyTables = 1u << 16;
+constexpr size_t kDedupBytes =
+    kDedupSlots * 4 + 3 * (size_t)kPreChunk * 4 + 256 + (size_t)kPreChunk * 80 + (size_t)kKeyTables * 81 * 16;
 // verify workspace for a grid of `grid` resident workgroups
 inline size_t verify_ws_bytes(uint32_t grid, bool dedup = false) {
   return kWsBytesPerBlock * grid + kPreBytes + (dedup ? kDedupBytes : 0);

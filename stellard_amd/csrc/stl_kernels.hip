@@ -238,9 +238,11 @@ __global__ __launch_bounds__(kBlock) void key_insert_kernel(const uint8_t* __res
 __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __restrict__ pk, uint32_t base,
                                                                const uint32_t* __restrict__ counter,
                                                                const uint32_t* __restrict__ owners,
-                                                               uint4* __restrict__ keytab) {
+                                                               uint4* __restrict__ keytab,
+                                                               uint4* __restrict__ keytabs) {
   const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
-  if (u >= *counter) return;  // no wave-level collective in this kernel
+  const uint32_t nu = *counter;
+  if (u >= nu) return;  // no wave-level collective in this kernel
   uint32_t A[8];
   ld8(A, pk + 32 * ((size_t)base + owners[u]));
   ge_p3 negA;
@@ -256,6 +258,11 @@ __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __
   uint4* q = keytab + (size_t)u * 5;
 #pragma unroll
   for (int i = 0; i < 5; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  if (nu <= kKeyTables) {  // the shared A-table: j*(-A), j = 0..8, as a lane would build it
+    ge_p3 P;
+    affine_to_p3(P, negA.X, negA.Y);
+    build_cached_table(TableView{keytabs + (size_t)u * kTableQuadsPerKey, 1}, P);
+  }
 }
 
 // Phase 1b with the keys already decoded: only R's square-root chain, so the
@@ -263,7 +270,7 @@ __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __
 __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
     const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk, uint32_t base, uint32_t cnt, uint32_t policy,
     uint4* __restrict__ pre, uint64_t* __restrict__ fb_words, const uint32_t* __restrict__ rep,
-    const uint32_t* __restrict__ uid_of, const uint4* __restrict__ keytab) {
+    const uint32_t* __restrict__ uid_of, const uint4* __restrict__ keytab, const uint32_t* __restrict__ counter) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   const bool live = t < cnt;
   const uint32_t tt = live ? t : cnt - 1;
@@ -272,7 +279,8 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   ld8(R, sig + 64 * j);
   ld8(S, sig + 64 * j + 32);
   ld8(A, pk + 32 * j);
-  const uint4* kq = keytab + (size_t)uid_of[rep[tt]] * 5;
+  const uint32_t uid = uid_of[rep[tt]];
+  const uint4* kq = keytab + (size_t)uid * 5;
   uint32_t kw[20];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -288,11 +296,16 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   uint4* q = pre + (size_t)tt * 14;
   HalfState h;
   uint32_t* w = reinterpret_cast<uint32_t*>(&h);
-  const uint4 q2 = q[kHalfTopsWord / 4];
+  const uint4 q2 = q[kHalfTopsWord / 4], q4 = q[4];
   w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+  w[16] = q4.x; w[17] = q4.y; w[18] = q4.z;
+  const uint32_t c_neg = h.tops & kHalfCNeg;
   verify_phase1_points_keyed(h, R, S, A, policy & 1u, nAx, nAy, kw[18] != 0);
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  h.pad = uid;
+  if (*counter <= kKeyTables) h.tops |= kHalfKeyed | c_neg;  // the main kernel reads the key's table
   if (live) {
+    q[4] = make_uint4(w[16], w[17], w[18], w[19]);
     q[kHalfTopsWord / 4] = make_uint4(w[8], w[9], w[10], w[11]);
 #pragma unroll
     for (int i = kHalfScalarQuads; i < 14; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
@@ -380,7 +393,8 @@ struct WideGlobal {
 #endif
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
-    uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr) {
+    uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
+    const uint4* __restrict__ keytabs) {
   uint4* slot = lane_slot(ws);
   const TableView tab1{slot, 1}, tab2{slot + kTableQuads, 1};
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -396,7 +410,7 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const bool live = t < cnt;
     HalfState h;
     ld_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
-    const bool ok = verify_phase2_half(h, tab1, tab2, wl) && live;
+    const bool ok = verify_phase2_half(h, tab1, tab2, wl, keytabs) && live;
     const uint64_t word = __ballot(ok);
     const uint32_t wbase = tile + wave * 64;
     if (lane == 0 && wbase < cnt) {
@@ -868,6 +882,7 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   uint32_t* owners = uid_of + kPreChunk;
   uint32_t* counter = owners + kPreChunk;
   uint4* keytab = reinterpret_cast<uint4*>(counter + 64);
+  uint4* keytabs = keytab + (size_t)kPreChunk * 5;
   for (uint64_t b64 = 0; b64 < n; b64 += kPreChunk) {  // 64-bit: n may reach 2^32 - 64
     const uint32_t base = (uint32_t)b64;
     const uint32_t cnt = n - base < kPreChunk ? n - base : kPreChunk;
@@ -887,14 +902,14 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(key_insert_kernel, g1, dim3(kBlock), 0, stream, pk, base, cnt, kslots, nslots - 1, rep, uid_of,
                          counter, owners);
-      hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, counter, owners, keytab);
+      hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, counter, owners, keytab, keytabs);
       hipLaunchKernelGGL(verify_point_kernel_keyed, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb,
-                         rep, uid_of, keytab);
+                         rep, uid_of, keytab, counter);
     } else {
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
     hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
-                       counters);
+                       counters, dedup ? keytabs : nullptr);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
                          policy, fb, bitmap, slots, counters);

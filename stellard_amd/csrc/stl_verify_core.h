@@ -80,6 +80,8 @@ STL_HD bool verify_prechecks(const uint32_t R[8], const uint32_t S[8], const uin
   return sc_lt_L(S) && !has_small_order(R) && point_is_canonical(A) && !has_small_order(A);
 }
 
+constexpr uint32_t kTableQuadsPerKey = 9 * 9;  // a 9-entry cached table, 9 x uint4 per entry
+
 // Per-lane table of cached multiples e*(-A), e = 0..8, 9 x uint4 per entry.
 // stride = distance (in uint4) between consecutive quads of one entry; the
 // kernel keeps each lane's 1296-byte table contiguous (stride 1).
@@ -332,6 +334,10 @@ constexpr uint32_t kHalfOk = 1u << 16;
 constexpr uint32_t kHalfFallback = 1u << 17;
 constexpr uint32_t kHalfCNeg = 1u << 18;
 constexpr uint32_t kHalfDNeg = 1u << 19;
+// STL_DEDUP_KEYS: the lane's key has a shared per-key table (multiples of -A,
+// cached form) at index `pad`; kHalfCNeg is kept so phase 2 can flip the
+// digit signs for P1 = +A.
+constexpr uint32_t kHalfKeyed = 1u << 20;
 
 // encode(P) == R is possible for some point P iff R is a canonical encoding:
 // y < p, and not "x == 0 with the sign bit set" (x == 0 <=> y == +-1).
@@ -525,12 +531,23 @@ struct WideHost {
 // with e's 16 radix-2^16 digits added from the wide tables at every fourth
 // position.  `Wide` reads table rows (WideHost here; the kernel's stages
 // them in LDS by asynchronous loads issued before the doublings).
+// With `keytabs` (STL_DEDUP_KEYS) a wave whose lanes all carry kHalfKeyed
+// reads the A-table from the shared per-key tables instead of building it.
 template <typename Wide>
-STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const TableView& tab2, Wide& wide) {
+STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const TableView& tab2, Wide& wide,
+                               const uint4* keytabs = nullptr) {
+  bool keyed = keytabs != nullptr && (p.tops & kHalfKeyed) != 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  keyed = __all(keyed);  // wave-uniform: the table source and the build are per wave
+#endif
+  const bool a_flip = keyed && (p.tops & kHalfCNeg) != 0;  // key table holds j*(-A); P1 = +A when c < 0
+  const TableView t1 = keyed ? TableView{const_cast<uint4*>(keytabs) + (size_t)p.pad * kTableQuadsPerKey, 1} : tab1;
   {
     ge_p3 P;
-    affine_to_p3(P, p.P1x, p.P1y);
-    build_cached_table(tab1, P);
+    if (!keyed) {
+      affine_to_p3(P, p.P1x, p.P1y);
+      build_cached_table(tab1, P);
+    }
     affine_to_p3(P, p.P2x, p.P2y);
     build_cached_table(tab2, P);
   }
@@ -584,16 +601,16 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     // hidden instead of stalling the adds.
     ge_cached ca, cq;
 #ifndef STL_NO_TABLE_PREFETCH
-    tab1.load(dc < 0 ? -dc : dc, ca);
+    t1.load(dc < 0 ? -dc : dc, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
 #endif
     if (bpos) wide.prefetch(de0, de1);
     if (i != npos - 1) dbl4(acc, acc2);
 #ifdef STL_NO_TABLE_PREFETCH
-    tab1.load(dc < 0 ? -dc : dc, ca);
+    t1.load(dc < 0 ? -dc : dc, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
 #endif
-    ge_cached_cneg(ca, dc < 0);
+    ge_cached_cneg(ca, (dc < 0) != a_flip);
     ge_add_cached(t, acc, ca);
     ge_p1p1_to_p3(acc, t);
     ge_cached_cneg(cq, dq < 0);

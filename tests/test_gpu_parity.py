@@ -500,3 +500,18 @@ def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
     assert np.array_equal(b1, ~bad)
     samp = rng.choice(n, 4000, replace=False)
     assert np.array_equal(b1[samp], oracle.verify_batch(s_np[samp], m_np[samp], p_np[samp], policy=policy & 1))
+    # more distinct keys in one chunk than shared key tables (2^16): the chunk
+    # falls back to per-lane A-tables and still gives the same bits
+    n2 = 70000
+    seeds2 = torch.from_numpy(rng.integers(0, 256, (n2, 32), dtype=np.uint8)).cuda()
+    msgs2 = torch.from_numpy(rng.integers(0, 256, (n2, 32), dtype=np.uint8)).cuda()
+    pk2, sig2 = stl.sign_batch_device(seeds2, msgs2)
+    s2 = sig2.cpu().numpy()
+    bad2 = rng.random(n2) < 0.05
+    s2[bad2, 3] ^= 0x01
+    d2 = [torch.from_numpy(s2).cuda(), msgs2, pk2]
+    u0 = stl.words_to_bool(stl.verify_batch_device(*d2, policy=policy), n2)
+    u1 = stl.words_to_bool(stl.verify_batch_device(*d2, policy=policy | stl.DEDUP_KEYS), n2)
+    torch.cuda.synchronize()
+    assert np.array_equal(u0, u1)
+    assert np.array_equal(u1, ~bad2)
