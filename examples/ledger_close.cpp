@@ -96,8 +96,9 @@ int main(int argc, char** argv) {
     std::memcpy(&sig[64 * i], txs[i].sig, 64);
     std::memcpy(&pk[32 * i], txs[i].pk, 32);
   }
+  // a ledger's signers repeat: decode each distinct key once (STL_DEDUP_KEYS)
   const int rc = stl_tx_verify_batch(pre.data(), off.data(), len.data(), sig.data(), pk.data(), n, bits.data(),
-                                     STL_POLICY_SODIUM_1_0_18);
+                                     STL_POLICY_SODIUM_1_0_18 | STL_DEDUP_KEYS);
   size_t good = 0;
   for (size_t i = 0; i < n; ++i) {
     if (rc == STL_OK && ((bits[i >> 3] >> (i & 7)) & 1)) {
