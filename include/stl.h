@@ -266,9 +266,21 @@ typedef struct stl_stats {
   uint64_t batches, signatures, errors;
   uint64_t host_ns, gather_ns;
   uint64_t accepted, full_length_lanes;
+  /* Phase timing (stl_set_phase_timing(1) or STL_PHASE_TIMING=1; zero when
+   * off): summed kernel time of the verify phases, measured with HIP events
+   * recorded on the launch stream between the phases of every chunk (at most
+   * 2^20 signatures) -- [0] scalar (SHA-512 + lattice), [1] point
+   * decompression (with the key-dedup kernels), [2] main (Straus loop),
+   * [3] fallback -- and the number of chunks timed. */
+  uint64_t phase_ns[4];
+  uint64_t phase_chunks;
 } stl_stats;
 int stl_get_stats(stl_stats *out);
 void stl_reset_stats(void);
+/* Enables (on != 0) or disables the phase timing of stl_stats for launches
+ * made after the call; returns the previous setting.  Off by default: two
+ * event records per phase and chunk. */
+int stl_set_phase_timing(int on);
 
 /* ---- testing hooks ----
  * Fault injection: after `calls` further HIP/RCCL calls made by libstl the

@@ -77,6 +77,7 @@ SYMBOLS = [
     ("stl_debug_fault_after", None, [ctypes.c_longlong]),
     ("stl_get_stats", ctypes.c_int, [_P]),
     ("stl_reset_stats", None, []),
+    ("stl_set_phase_timing", ctypes.c_int, [ctypes.c_int]),
     ("stl_debug_verify_k_device", ctypes.c_int, [_U8P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
 ]
 

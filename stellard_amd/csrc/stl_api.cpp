@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -130,6 +131,96 @@ struct DevBuf {
   }
 };
 
+// Phase timing (stl_set_phase_timing): launch_verify marks the phase
+// boundaries of each chunk; each mark records a pooled HIP event on the launch
+// stream.  stl_get_stats sums the completed chunks' phase durations.  Timing
+// calls bypass the fault-injection countdown and never fail a launch: a chunk
+// whose events could not be recorded is dropped from the sums.
+struct PhaseTimer {
+  std::mutex mu;
+  std::vector<hipEvent_t> pool;
+  std::vector<std::array<hipEvent_t, 5>> done;
+  uint64_t ns[4] = {0, 0, 0, 0};
+  uint64_t chunks = 0;
+  hipEvent_t take() {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+    return e;
+  }
+  void give(hipEvent_t e) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(mu);
+    pool.push_back(e);
+  }
+  // completed chunks -> sums (the caller has synchronised the device)
+  void collect() {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& c : done) {
+      uint64_t t[4];
+      bool ok = true;
+      for (int i = 0; i < 4 && ok; ++i) {
+        float ms = 0.f;
+        ok = hipEventElapsedTime(&ms, c[i], c[i + 1]) == hipSuccess;
+        t[i] = (uint64_t)((double)ms * 1e6);
+      }
+      if (ok) {
+        for (int i = 0; i < 4; ++i) ns[i] += t[i];
+        ++chunks;
+      }
+      for (hipEvent_t e : c) pool.push_back(e);
+    }
+    done.clear();
+  }
+  void reset() {
+    collect();
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& v : ns) v = 0;
+    chunks = 0;
+  }
+  void release() {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& c : done)
+      for (hipEvent_t e : c) pool.push_back(e);
+    done.clear();
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    pool.clear();
+  }
+};
+
+std::atomic<bool> g_phase_timing{false};
+
+// one chunk being marked by this thread (marks of a chunk come from one thread)
+thread_local std::array<hipEvent_t, 5> t_marks;
+thread_local bool t_marks_ok = false;
+
+void phase_mark(void* ctx, hipStream_t s, int i) {
+  auto* t = static_cast<PhaseTimer*>(ctx);
+  if (i == 0) t_marks_ok = true;
+  hipEvent_t e = t->take();
+  if (!e || hipEventRecord(e, s) != hipSuccess) {
+    t->give(e);
+    t_marks[i] = nullptr;
+    t_marks_ok = false;
+  } else {
+    t_marks[i] = e;
+  }
+  if (i == 4) {
+    if (t_marks_ok) {
+      std::lock_guard<std::mutex> lk(t->mu);
+      t->done.push_back(t_marks);
+    } else {
+      for (hipEvent_t m : t_marks) t->give(m);
+    }
+    t_marks_ok = false;
+  }
+}
+
 struct Device {
   int ordinal = 0;
   int cus = 0;
@@ -143,7 +234,12 @@ struct Device {
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;  // tx-hash work counter
   std::mutex ws_mu;
+  PhaseTimer timer;
+  stl::PhaseClock clock{phase_mark, &timer};
 };
+
+// the device's phase clock when timing is on, else none
+const stl::PhaseClock* phase_clock(Device& d) { return g_phase_timing.load() ? &d.clock : nullptr; }
 
 std::mutex g_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
@@ -229,6 +325,7 @@ void release_device(Device& d) {
     b->release();
   for (auto& kv : d.stream_ws) kv.second->release();
   for (auto& kv : d.stream_ctr) kv.second->release();
+  d.timer.release();
   if (d.stream) (void)hipStreamDestroy(d.stream);
   if (d.copy) (void)hipStreamDestroy(d.copy);
   d.stream = d.copy = nullptr;
@@ -429,7 +526,7 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
     STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
                                static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, static_cast<uint4*>(d.ws.p),
                                grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream,
-                               dev_counters(d)));
+                               dev_counters(d), phase_clock(d)));
   }
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
   if (dtxid) STL_TRY(hipMemcpyAsync(b.txid + 32 * lo, dtxid, n * 32, hipMemcpyDeviceToHost, d.stream));
@@ -584,6 +681,7 @@ int stl_init(const stl_config* cfg) {
   const char* fa = std::getenv("STL_FAULT_AFTER");
   if (fa && *fa) g_fault_after.store(std::atoll(fa));
   g_trace = env_int("STL_TRACE", 0) != 0;
+  if (env_int("STL_PHASE_TIMING", 0) != 0) g_phase_timing.store(true);
   int first = 0, want = -1, spd = 1;
   uint32_t cflags = 0;
   if (cfg) {  // argument checks first: they need no device
@@ -685,6 +783,8 @@ int stl_get_stats(stl_stats* out) {
   out->gather_ns = g_st_gather_ns.load();
   out->accepted = 0;
   out->full_length_lanes = 0;
+  for (auto& v : out->phase_ns) v = 0;
+  out->phase_chunks = 0;
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& d : g_devs) {  // device counters: waits for the work queued before the call
     if (!d->counters.p) continue;
@@ -694,6 +794,10 @@ int stl_get_stats(stl_stats* out) {
       return STL_EHIP;
     out->accepted += c[0];
     out->full_length_lanes += c[1];
+    d->timer.collect();
+    std::lock_guard<std::mutex> tl(d->timer.mu);
+    for (int i = 0; i < 4; ++i) out->phase_ns[i] += d->timer.ns[i];
+    out->phase_chunks += d->timer.chunks;
   }
   return STL_OK;
 }
@@ -706,8 +810,14 @@ void stl_reset_stats(void) {
   g_st_gather_ns = 0;
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& d : g_devs)
-    if (d->counters.p && hipSetDevice(d->ordinal) == hipSuccess) (void)hipMemset(d->counters.p, 0, 64);
+    if (d->counters.p && hipSetDevice(d->ordinal) == hipSuccess) {
+      (void)hipMemset(d->counters.p, 0, 64);
+      (void)hipDeviceSynchronize();  // queued chunks complete before their events are read and dropped
+      d->timer.reset();
+    }
 }
+
+int stl_set_phase_timing(int on) { return g_phase_timing.exchange(on != 0) ? 1 : 0; }
 
 void stl_shard_range(size_t n, int r, int g, size_t* lo, size_t* hi) {
   if (!lo || !hi) return;
@@ -812,7 +922,7 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
     STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                                static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
                                STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true,
-                               static_cast<const uint4*>(d.wide.p), s, dev_counters(d)));
+                               static_cast<const uint4*>(d.wide.p), s, dev_counters(d), phase_clock(d)));
     STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
     STL_TRY(hipStreamSynchronize(s));
     return STL_OK;
@@ -845,7 +955,8 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   uint4* ws = nullptr;
   STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d)));
+                             grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
+                             phase_clock(*d)));
   return STL_OK;
 }
 
@@ -861,7 +972,8 @@ int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const ui
   uint4* ws = nullptr;
   STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_k, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d)));
+                             grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
+                             phase_clock(*d)));
   return STL_OK;
 }
 

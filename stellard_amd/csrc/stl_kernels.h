@@ -41,9 +41,17 @@ inline uint32_t kernel_mode(uint32_t flags) {
 const void* kernel_verify_msg32();
 // counters (nullable): device u64 [0] accept bits written, [1] lanes checked by
 // the full-length fallback path (stl_get_stats)
+// Optional phase clock (stl_set_phase_timing): launch_verify calls
+// mark(ctx, stream, i) before a chunk's first kernel (i = 0) and after each
+// phase -- 1 scalar, 2 point (+ the key-dedup kernels), 3 main, 4 fallback.
+struct PhaseClock {
+  void (*mark)(void* ctx, hipStream_t stream, int i);
+  void* ctx;
+};
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k, const uint4* wide,
-                         hipStream_t stream, unsigned long long* counters = nullptr);
+                         hipStream_t stream, unsigned long long* counters = nullptr,
+                         const PhaseClock* clock = nullptr);
 hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t* m, const uint64_t* moff,
                            const uint64_t* mlen, uint32_t n, uint8_t* k_out, hipStream_t stream);
 // counter: one device word of scratch (reset by the launcher); grid: upper

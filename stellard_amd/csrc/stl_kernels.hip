@@ -867,8 +867,12 @@ hipError_t launch_wide_table(uint4* out, hipStream_t stream) {
 
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
-                         const uint4* wide, hipStream_t stream, unsigned long long* counters) {
+                         const uint4* wide, hipStream_t stream, unsigned long long* counters,
+                         const PhaseClock* clock) {
   if (n == 0) return hipSuccess;
+  auto mark = [&](int i) {
+    if (clock) clock->mark(clock->ctx, stream, i);
+  };
   // ws = [per-lane slots: grid x kWsBytesPerBlock][HalfState x kPreChunk][fallback words]
   //      [dedup (kModeDedupKeys): slots, rep, uid_of, owners, counter, decoded keys]
   uint4* slots = ws;
@@ -889,10 +893,12 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     const dim3 g1((cnt + kBlock - 1) / kBlock);
     const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
     const dim3 g2(tiles < grid ? tiles : grid);
+    mark(0);
     if (pre_k)
       hipLaunchKernelGGL(verify_scalar_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     else
       hipLaunchKernelGGL(verify_scalar_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
+    mark(1);
     if (dedup) {
       uint32_t nslots = 64;
       while (nslots < 2 * cnt) nslots <<= 1;  // <= kDedupSlots
@@ -908,14 +914,17 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     } else {
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
+    mark(2);
     hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
                        counters, dedup ? keytabs : nullptr);
+    mark(3);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
                          policy, fb, bitmap, slots, counters);
     else
       hipLaunchKernelGGL(verify_fallback_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
                          policy, fb, bitmap, slots, counters);
+    mark(4);
   }
   return hipGetLastError();
 }

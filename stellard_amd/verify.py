@@ -420,18 +420,33 @@ class Stats(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
                 ("batches", ctypes.c_uint64), ("signatures", ctypes.c_uint64), ("errors", ctypes.c_uint64),
                 ("host_ns", ctypes.c_uint64), ("gather_ns", ctypes.c_uint64),
-                ("accepted", ctypes.c_uint64), ("full_length_lanes", ctypes.c_uint64)]
+                ("accepted", ctypes.c_uint64), ("full_length_lanes", ctypes.c_uint64),
+                ("phase_ns", ctypes.c_uint64 * 4), ("phase_chunks", ctypes.c_uint64)]
+
+
+PHASES = ("scalar", "point", "main", "fallback")
 
 
 def get_stats():
+    """Counters of include/stl.h stl_get_stats; ``phase_ns`` is a dict of the
+    summed kernel time per verify phase (zero unless phase timing is on)."""
     st = Stats()
     st.struct_size = ctypes.sizeof(Stats)
     N.check(N.load().stl_get_stats(ctypes.byref(st)), "stl_get_stats")
-    return {name: getattr(st, name) for name, _ in Stats._fields_ if name not in ("struct_size", "reserved")}
+    out = {name: getattr(st, name) for name, _ in Stats._fields_
+           if name not in ("struct_size", "reserved", "phase_ns")}
+    out["phase_ns"] = dict(zip(PHASES, list(st.phase_ns)))
+    return out
 
 
 def reset_stats():
     N.load().stl_reset_stats()
+
+
+def set_phase_timing(on):
+    """Per-phase HIP-event timing of the verify launches (stl_set_phase_timing);
+    returns the previous setting."""
+    return bool(N.load().stl_set_phase_timing(1 if on else 0))
 
 
 # ---- testing hooks ----

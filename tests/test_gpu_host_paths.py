@@ -306,6 +306,33 @@ def test_stats_count_calls_signatures_and_errors(stl, golden):
     assert st["batches"] == 2 and st["errors"] == 1
 
 
+def test_phase_timing(stl, golden, torch_cuda):
+    """stl_set_phase_timing: per-phase event times for every chunk of the
+    host and device entry points, the same bits with timing on, and nothing
+    timed once it is off again."""
+    torch = torch_cuda
+    sig, msg, pk, exp = _golden_rows(golden, 3000, seed=9)
+    stl.reset_stats()
+    assert stl.set_phase_timing(True) is False
+    try:
+        assert np.array_equal(stl.verify_batch(sig, msg, pk), exp)
+        d = [torch.from_numpy(a).cuda() for a in (sig, msg, pk)]
+        w = stl.verify_batch_device(*d)
+        torch.cuda.synchronize()
+        assert np.array_equal(stl.words_to_bool(w, 3000), exp)
+        st = stl.get_stats()
+        assert st["phase_chunks"] == 2, st
+        ph = st["phase_ns"]
+        assert all(ph[k] > 0 for k in ("scalar", "point", "main")), ph
+        assert ph["main"] > ph["scalar"], ph
+    finally:
+        stl.set_phase_timing(False)
+    stl.verify_batch(sig, msg, pk)
+    assert stl.get_stats()["phase_chunks"] == 2
+    stl.reset_stats()
+    assert stl.get_stats()["phase_chunks"] == 0
+
+
 def test_fault_injection_batcher_delivers_errors(stl, oracle, golden):
     sig, msg, pk, exp = _golden_rows(golden, 50, seed=4)
     for k in (0, 2, 5):

@@ -220,3 +220,7 @@ def test_stats_without_gpu():
     bad = V.Stats()
     bad.struct_size = 8
     assert N.load().stl_get_stats(ctypes.byref(bad)) == N.STL_EINVAL
+    assert st["phase_chunks"] == 0 and set(st["phase_ns"]) == {"scalar", "point", "main", "fallback"}
+    # the phase-timing switch returns the previous setting
+    assert V.set_phase_timing(True) is False
+    assert V.set_phase_timing(False) is True

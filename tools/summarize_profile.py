@@ -65,10 +65,22 @@ summary = {"kernels": per, "verify_launch_sequence": tot,
            "other_kernels": {k: v for k, v in stats.items() if "verify" not in k}}
 json.dump(summary, open(os.path.join(d, "summary.json"), "w"), indent=1)
 if "--traffic" in sys.argv:
-    json.dump({"source": f"{d}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, summed "
+    traffic = {"source": f"{d}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, summed "
                          "over the verify_scalar/point/main/fallback kernels, one verify launch sequence of the bench batch)",
                "hbm_bytes_per_launch": tot["hbm_bytes_per_launch"],
                "hbm_bytes_per_launch_fetch_x2_upper": tot["hbm_bytes_per_launch_fetch_x2_upper"],
-               "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, raw; FETCH x2 (gfx950 wide-read correction) upper bound"},
-              open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w"), indent=1)
+               "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, raw; FETCH x2 (gfx950 wide-read correction) upper bound"}
+    m = summary["kernels"].get("stl::verify_main_kernel")
+    if m:  # the dominant kernel, as bench.py's roofline reports it
+        traffic["main_kernel"] = {
+            "kernel": "stl::verify_main_kernel",
+            "fetch_size_bytes_raw": m["fetch_bytes_raw"], "write_size_bytes": m["write_bytes"],
+            "hbm_bytes_per_launch": 2 * m["fetch_bytes_raw"] + m["write_bytes"],
+            "correction": "MI355X_MICROARCH.md HBM section: FETCH_SIZE reports half the bytes of 16-B/lane reads "
+                          "on gfx950 (all of this kernel's global reads are 16-B/lane uint4 table loads and "
+                          "global_load_lds rows), so 2 x FETCH_SIZE + WRITE_SIZE",
+            "avg_ns_rocprof": m["trace"]["avg_ns"]}
+    for path in (os.path.join(ROOT, "profiles", "traffic_latest.json"), os.path.join(d, "traffic_latest.json")):
+        with open(path, "w") as f:
+            json.dump(traffic, f, indent=1)
 print(json.dumps(summary, indent=1))
