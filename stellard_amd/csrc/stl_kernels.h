@@ -23,8 +23,12 @@ constexpr size_t kDedupSlots = 2 * (size_t)kPreChunk;
 // shared per-key A-tables (9 cached entries, 1,296 B) for up to kKeyTables
 // distinct keys per chunk; above that the chunk builds per-lane tables
 constexpr uint32_t kKeyTables = 1u << 16;
-constexpr size_t kDedupBytes =
-    kDedupSlots * 4 + 3 * (size_t)kPreChunk * 4 + 256 + (size_t)kPreChunk * 80 + (size_t)kKeyTables * 81 * 16;
+// wide shared A-tables (137 cached entries, 19,728 B) when a chunk has at most
+// kWideKeys distinct keys and at least kWideKeyRepeat signatures per key
+constexpr uint32_t kWideKeys = 4096;
+constexpr uint32_t kWideKeyRepeat = 32;
+constexpr size_t kDedupBytes = kDedupSlots * 4 + 3 * (size_t)kPreChunk * 4 + 256 + (size_t)kPreChunk * 80 +
+                               (size_t)kKeyTables * 81 * 16 + (size_t)kWideKeys * 137 * 9 * 16;
 // verify workspace for a grid of `grid` resident workgroups
 inline size_t verify_ws_bytes(uint32_t grid, bool dedup = false) {
   return kWsBytesPerBlock * grid + kPreBytes + (dedup ? kDedupBytes : 0);

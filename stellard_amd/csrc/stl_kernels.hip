@@ -176,7 +176,11 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_point_k
 //                       kKeyProbes probes: a lane that finds no slot (a
 //                       crowded or adversarial table) owns its own key, so the
 //                       work per lane stays bounded;
-//   key_decode_kernel   one lane per distinct key: the square-root chain of -A;
+//   key_decode_kernel   one lane per distinct key: the square-root chain of -A,
+//                       and the key's 9-entry table;
+//   key_table_wide_kernel  few keys, many signatures each (kWideKeys,
+//                       kWideKeyRepeat): one lane per (key, j), j*(-A) for
+//                       j = 0..136, the table of c's radix-256 digit pairs;
 //   verify_point_kernel_keyed  the point half with only R decoded.
 constexpr uint32_t kKeyEmpty = 0xffffffffu;
 constexpr int kKeyProbes = 32;
@@ -235,11 +239,16 @@ __global__ __launch_bounds__(kBlock) void key_insert_kernel(const uint8_t* __res
   }
 }
 
+// the chunk's keys get the wide tables (wave-uniform: one chunk per launch)
+__device__ __forceinline__ bool wide_keys(uint32_t nu, uint32_t cnt) {
+  return nu <= kWideKeys && (uint64_t)nu * kWideKeyRepeat <= cnt;
+}
+
 __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __restrict__ pk, uint32_t base,
                                                                const uint32_t* __restrict__ counter,
                                                                const uint32_t* __restrict__ owners,
                                                                uint4* __restrict__ keytab,
-                                                               uint4* __restrict__ keytabs) {
+                                                               uint4* __restrict__ keytabs, uint32_t cnt) {
   const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t nu = *counter;
   if (u >= nu) return;  // no wave-level collective in this kernel
@@ -258,11 +267,57 @@ __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __
   uint4* q = keytab + (size_t)u * 5;
 #pragma unroll
   for (int i = 0; i < 5; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
-  if (nu <= kKeyTables) {  // the shared A-table: j*(-A), j = 0..8, as a lane would build it
+  if (nu <= kKeyTables && !wide_keys(nu, cnt)) {  // the shared A-table: j*(-A), j = 0..8, as a lane would build it
     ge_p3 P;
     affine_to_p3(P, negA.X, negA.Y);
     build_cached_table(TableView{keytabs + (size_t)u * kTableQuadsPerKey, 1}, P);
   }
+}
+
+// One lane per (key u, multiple j): j*(-A) by double-and-add over j's 8 bits
+// from the decoded key, stored in cached form (a table row as
+// build_cached_table writes it).  Exits unless the chunk is in wide mode.
+__global__ __launch_bounds__(kBlock) void key_table_wide_kernel(const uint32_t* __restrict__ counter, uint32_t cnt,
+                                                                const uint4* __restrict__ keytab,
+                                                                uint4* __restrict__ widetabs) {
+  const uint32_t nu = *counter;
+  if (!wide_keys(nu, cnt)) return;
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t u = g / (uint32_t)kWideKeyEntries, j = g % (uint32_t)kWideKeyEntries;
+  if (u >= nu) return;  // no wave-level collective in this kernel
+  const uint4* kq = keytab + (size_t)u * 5;
+  uint32_t kw[20];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint4 v = kq[i];
+    kw[4 * i] = v.x; kw[4 * i + 1] = v.y; kw[4 * i + 2] = v.z; kw[4 * i + 3] = v.w;
+  }
+  fe x, y;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    x.v[i] = kw[i];
+    y.v[i] = kw[9 + i];
+  }
+  ge_p3 P, acc;
+  affine_to_p3(P, x, y);
+  ge_cached cP;
+  ge_p3_to_cached(cP, P);
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_p2 a2;
+#pragma unroll 1
+  for (int b = 7; b >= 0; --b) {
+    ge_p3_to_p2(a2, acc);
+    ge_p2_dbl(t, a2);
+    ge_p1p1_to_p3(acc, t);
+    if ((j >> b) & 1u) {
+      ge_add_cached(t, acc, cP);
+      ge_p1p1_to_p3(acc, t);
+    }
+  }
+  ge_cached c;
+  ge_p3_to_cached(c, acc);
+  TableView{widetabs + (size_t)u * (kWideKeyEntries * 9), 1}.store((int)j, c);
 }
 
 // Phase 1b with the keys already decoded: only R's square-root chain, so the
@@ -303,7 +358,9 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   verify_phase1_points_keyed(h, R, S, A, policy & 1u, nAx, nAy, kw[18] != 0);
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
   h.pad = uid;
-  if (*counter <= kKeyTables) h.tops |= kHalfKeyed | c_neg;  // the main kernel reads the key's table
+  const uint32_t nu = *counter;
+  if (nu <= kKeyTables) h.tops |= kHalfKeyed | c_neg;  // the main kernel reads the key's table
+  if (wide_keys(nu, cnt)) h.tops |= kHalfKeyedWide;
   if (live) {
     q[4] = make_uint4(w[16], w[17], w[18], w[19]);
     q[kHalfTopsWord / 4] = make_uint4(w[8], w[9], w[10], w[11]);
@@ -394,7 +451,7 @@ struct WideGlobal {
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
     uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
-    const uint4* __restrict__ keytabs) {
+    const uint4* __restrict__ keytabs, const uint4* __restrict__ widetabs) {
   uint4* slot = lane_slot(ws);
   const TableView tab1{slot, 1}, tab2{slot + kTableQuads, 1};
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -410,7 +467,7 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const bool live = t < cnt;
     HalfState h;
     ld_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
-    const bool ok = verify_phase2_half(h, tab1, tab2, wl, keytabs) && live;
+    const bool ok = verify_phase2_half(h, tab1, tab2, wl, keytabs, widetabs) && live;
     const uint64_t word = __ballot(ok);
     const uint32_t wbase = tile + wave * 64;
     if (lane == 0 && wbase < cnt) {
@@ -887,6 +944,7 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   uint32_t* counter = owners + kPreChunk;
   uint4* keytab = reinterpret_cast<uint4*>(counter + 64);
   uint4* keytabs = keytab + (size_t)kPreChunk * 5;
+  uint4* widetabs = keytabs + (size_t)kKeyTables * kTableQuadsPerKey;
   for (uint64_t b64 = 0; b64 < n; b64 += kPreChunk) {  // 64-bit: n may reach 2^32 - 64
     const uint32_t base = (uint32_t)b64;
     const uint32_t cnt = n - base < kPreChunk ? n - base : kPreChunk;
@@ -908,7 +966,12 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(key_insert_kernel, g1, dim3(kBlock), 0, stream, pk, base, cnt, kslots, nslots - 1, rep, uid_of,
                          counter, owners);
-      hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, counter, owners, keytab, keytabs);
+      hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, counter, owners, keytab, keytabs,
+                         cnt);
+      const uint32_t wmax = cnt / kWideKeyRepeat < kWideKeys ? cnt / kWideKeyRepeat : kWideKeys;  // keys that can be wide
+      if (wmax > 0)
+        hipLaunchKernelGGL(key_table_wide_kernel, dim3((wmax * (uint32_t)kWideKeyEntries + kBlock - 1) / kBlock),
+                           dim3(kBlock), 0, stream, counter, cnt, keytab, widetabs);
       hipLaunchKernelGGL(verify_point_kernel_keyed, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb,
                          rep, uid_of, keytab, counter);
     } else {
@@ -916,7 +979,7 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     }
     mark(2);
     hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
-                       counters, dedup ? keytabs : nullptr);
+                       counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr);
     mark(3);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,

@@ -338,6 +338,11 @@ constexpr uint32_t kHalfDNeg = 1u << 19;
 // cached form) at index `pad`; kHalfCNeg is kept so phase 2 can flip the
 // digit signs for P1 = +A.
 constexpr uint32_t kHalfKeyed = 1u << 20;
+// ... and the key also has a wide shared table (j*(-A), j = 0..136, cached
+// form): c's digits are taken in pairs as signed radix-256 digits, one A-add
+// every second position.
+constexpr uint32_t kHalfKeyedWide = 1u << 21;
+constexpr int kWideKeyEntries = 137;  // |16*d1 + d0| <= 136 for signed radix-16 digits |d| <= 8
 
 // encode(P) == R is possible for some point P iff R is a canonical encoding:
 // y < p, and not "x == 0 with the sign bit set" (x == 0 <=> y == +-1).
@@ -532,16 +537,23 @@ struct WideHost {
 // position.  `Wide` reads table rows (WideHost here; the kernel's stages
 // them in LDS by asynchronous loads issued before the doublings).
 // With `keytabs` (STL_DEDUP_KEYS) a wave whose lanes all carry kHalfKeyed
-// reads the A-table from the shared per-key tables instead of building it.
+// reads the A-table from the shared per-key tables instead of building it;
+// with `widetabs` and kHalfKeyedWide on every lane it adds c's digits in pairs
+// (16*d_{2j+1} + d_{2j} at position 2j) from the key's 137-entry table.
 template <typename Wide>
 STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const TableView& tab2, Wide& wide,
-                               const uint4* keytabs = nullptr) {
+                               const uint4* keytabs = nullptr, const uint4* widetabs = nullptr) {
   bool keyed = keytabs != nullptr && (p.tops & kHalfKeyed) != 0;
+  bool kwide = keyed && widetabs != nullptr && (p.tops & kHalfKeyedWide) != 0;
 #if defined(__HIP_DEVICE_COMPILE__)
   keyed = __all(keyed);  // wave-uniform: the table source and the build are per wave
+  kwide = __all(kwide);
 #endif
+  kwide = kwide && keyed;
   const bool a_flip = keyed && (p.tops & kHalfCNeg) != 0;  // key table holds j*(-A); P1 = +A when c < 0
-  const TableView t1 = keyed ? TableView{const_cast<uint4*>(keytabs) + (size_t)p.pad * kTableQuadsPerKey, 1} : tab1;
+  const TableView t1 =
+      kwide ? TableView{const_cast<uint4*>(widetabs) + (size_t)p.pad * (kWideKeyEntries * 9), 1}
+            : keyed ? TableView{const_cast<uint4*>(keytabs) + (size_t)p.pad * kTableQuadsPerKey, 1} : tab1;
   {
     ge_p3 P;
     if (!keyed) {
@@ -566,6 +578,7 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
   ge_p3_0(acc);
   ge_p2_0(acc2);
   uint32_t wc = 0, wd = 0, we0 = 0, we1 = 0;
+  int cprev = 0;  // kwide: c's digit of the odd position above, added with the next even one
 #pragma unroll 1
   for (int i = kHalfDigits - 1; i >= 0; --i) {
     if ((i & 7) == 7) {  // next 8 radix-16 digits of |c| and |d|
@@ -586,9 +599,20 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
         ed[4 + m] = ed[4 + m - 1];
       }
     }
-    const int dc = (int32_t)wc >> 28, dq = (int32_t)wd >> 28;
+    int dc = (int32_t)wc >> 28;
+    const int dq = (int32_t)wd >> 28;
     wc <<= 4;
     wd <<= 4;
+    bool cadd = true;  // wave-uniform
+    if (kwide) {
+      if (i & 1) {
+        cprev = dc;
+        cadd = false;
+      } else {
+        dc += 16 * cprev;
+        cprev = 0;
+      }
+    }
     const bool bpos = (i & 3) == 0 && i < 32;  // wave-uniform
     int de0 = 0, de1 = 0;
     if (bpos) {
@@ -601,18 +625,20 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     // hidden instead of stalling the adds.
     ge_cached ca, cq;
 #ifndef STL_NO_TABLE_PREFETCH
-    t1.load(dc < 0 ? -dc : dc, ca);
+    if (cadd) t1.load(dc < 0 ? -dc : dc, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
 #endif
     if (bpos) wide.prefetch(de0, de1);
     if (i != npos - 1) dbl4(acc, acc2);
 #ifdef STL_NO_TABLE_PREFETCH
-    t1.load(dc < 0 ? -dc : dc, ca);
+    if (cadd) t1.load(dc < 0 ? -dc : dc, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
 #endif
-    ge_cached_cneg(ca, (dc < 0) != a_flip);
-    ge_add_cached(t, acc, ca);
-    ge_p1p1_to_p3(acc, t);
+    if (cadd) {
+      ge_cached_cneg(ca, (dc < 0) != a_flip);
+      ge_add_cached(t, acc, ca);
+      ge_p1p1_to_p3(acc, t);
+    }
     ge_cached_cneg(cq, dq < 0);
     ge_add_cached(t, acc, cq);
     if (!bpos) {

@@ -118,6 +118,22 @@ class Gpu:
             times.append(a.elapsed_time(b) * 1e-3)
         return self.V.words_to_bool(words, sig.shape[0]), float(np.median(times))
 
+    def phase_split(self, fn, reps=3):
+        """ms per verify chunk (<= 2^20 signatures) of each verify phase, from
+        libstl's phase clock (HIP events between the kernels) over `reps` calls."""
+        V = self.V
+        V.set_phase_timing(True)
+        V.reset_stats()
+        try:
+            for _ in range(reps):
+                fn()
+            self.torch.cuda.synchronize()
+            st = V.get_stats()
+        finally:
+            V.set_phase_timing(False)
+        c = max(1, st["phase_chunks"])
+        return {k: v / c / 1e6 for k, v in st["phase_ns"].items()}
+
     def tx_hash_dev(self, d_blob, d_off, d_len, n, d_msg):
         N = self.N
         N.check(N.load().stl_tx_hash_batch_device(
@@ -237,6 +253,9 @@ def tx_config(gpu, cpu, n, rng, pad_lens, cpu_samples):
         times.append(a.elapsed_time(b) * 1e-3)
     dedup_bits = gpu.V.words_to_bool(words, n)
     dedup_s = float(np.median(times[1:]))
+    phase = gpu.phase_split(lambda: gpu.V.verify_batch_device(sig, d_msg, pk, out_words=words, stream=gpu.stream))
+    phase_dd = gpu.phase_split(lambda: gpu.V.verify_batch_device(sig, d_msg, pk, out_words=words, stream=gpu.stream,
+                                                                 policy=gpu.V.DEDUP_KEYS))
     # host API (PCIe-inclusive): one stl_tx_verify_batch call on packed host buffers
     bm = np.zeros((n + 7) // 8, np.uint8)
     B = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
@@ -258,6 +277,7 @@ def tx_config(gpu, cpu, n, rng, pad_lens, cpu_samples):
                                    "total": int(lens.sum())},
         "gpu_device_resident_tx_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
         "gpu_device_resident_dedup_keys_tx_per_s": n / dedup_s, "gpu_device_dedup_keys_ms": dedup_s * 1e3,
+        "gpu_phase_ms": phase, "gpu_phase_ms_dedup_keys": phase_dd,
         "gpu_host_api_tx_per_s": n / host_s,
         "cpu_reference": cpu_rates(run, n, cpu_samples),
         "bitmap_parity": {"rows": n, "mismatches_device": int((dev_bits != ref_bits).sum()),
@@ -346,6 +366,9 @@ def config2(gpu, cpu):
     d_msg = t.from_numpy(msgs).cuda()
     bits, dev_s = gpu.verify_dev(sig, d_msg, pk)
     dbits, dedup_s = gpu.verify_dev(sig, d_msg, pk, policy=gpu.V.DEDUP_KEYS)  # all keys distinct: overhead only
+    phase = gpu.phase_split(lambda: gpu.V.verify_batch_device(sig, d_msg, pk, stream=gpu.stream))
+    phase_dd = gpu.phase_split(lambda: gpu.V.verify_batch_device(sig, d_msg, pk, stream=gpu.stream,
+                                                                 policy=gpu.V.DEDUP_KEYS))
     s_np, p_np = sig.cpu().numpy(), pk.cpu().numpy()
     hb, host_s = timed(lambda: gpu.V.verify_batch(s_np, msgs, p_np))
     hb, host_s = timed(lambda: gpu.V.verify_batch(s_np, msgs, p_np))
@@ -357,6 +380,7 @@ def config2(gpu, cpu):
     ref = run(0, sample, 16)
     return {"n": n, "gpu_device_resident_verifies_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
             "gpu_device_dedup_keys_ms_all_distinct": dedup_s * 1e3, "dedup_bits_equal": bool((dbits == bits).all()),
+            "gpu_phase_ms": phase, "gpu_phase_ms_dedup_keys_all_distinct": phase_dd,
             "gpu_host_api_verifies_per_s": n / host_s,
             "cpu_reference": cpu_rates(run, n, [(16, 1 << 19), (6, 1 << 18), (1, 1 << 15)]),
             "bitmap_parity": {"rows": sample, "mismatches": int((bits[:sample] != ref).sum()),
