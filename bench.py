@@ -87,6 +87,9 @@ def launch(args):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
+    # one node (--nnodes=1): RCCL's bootstrap sockets stay on loopback, so an
+    # unresolvable hostname or a down NIC cannot stall ncclCommInitRank
+    env.setdefault("NCCL_SOCKET_IFNAME", "lo")
     return subprocess.call(cmd, env=env)
 
 
