@@ -201,7 +201,15 @@ thread_local bool t_marks_ok = false;
 
 void phase_mark(void* ctx, hipStream_t s, int i) {
   auto* t = static_cast<PhaseTimer*>(ctx);
-  if (i == 0) t_marks_ok = true;
+  if (i == 0) {
+    // events left by a chunk whose launches stopped between its marks (their
+    // timer may be gone after stl_shutdown): destroy them
+    for (hipEvent_t& m : t_marks) {
+      if (m) (void)hipEventDestroy(m);
+      m = nullptr;
+    }
+    t_marks_ok = true;
+  }
   hipEvent_t e = t->take();
   if (!e || hipEventRecord(e, s) != hipSuccess) {
     t->give(e);
@@ -217,6 +225,7 @@ void phase_mark(void* ctx, hipStream_t s, int i) {
     } else {
       for (hipEvent_t m : t_marks) t->give(m);
     }
+    t_marks.fill(nullptr);
     t_marks_ok = false;
   }
 }
