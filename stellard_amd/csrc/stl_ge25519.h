@@ -14,6 +14,13 @@ struct ge_p1p1 { fe X, Y, Z, T; };
 struct ge_cached { fe YpX, YmX, Z, T2d; };
 struct ge_niels { fe ypx, ymx, xy2d; };
 
+// Products interleaved per group formula: 4 (default; 3-4 independent mad
+// chains per wave, for 2 waves/SIMD) or 2 (fewer live registers, for kernels
+// that run more waves per SIMD).
+#ifndef STL_GE_NOPS
+#define STL_GE_NOPS 4
+#endif
+
 STL_HD void ge_p2_0(ge_p2& h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); }
 STL_HD void ge_p3_0(ge_p3& h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); fe_0(h.T); }
 STL_HD void ge_cached_0(ge_cached& h) { fe_1(h.YpX); fe_1(h.YmX); fe_1(h.Z); fe_0(h.T2d); }
@@ -22,7 +29,12 @@ STL_HD void ge_cached_0(ge_cached& h) { fe_1(h.YpX); fe_1(h.YmX); fe_1(h.Z); fe_
 // T [1]: X*T <= 3, Y*Z <= 6, Z*T <= 3, X*Y <= 6 (fe_mul needs <= 7).
 STL_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
   fe X, Y, Z;
+#if STL_GE_NOPS == 2
+  fe_mul2(X, p.X, p.T, Y, p.Y, p.Z);
+  fe_mul(Z, p.Z, p.T);
+#else
   fe_mul3(X, p.X, p.T, Y, p.Y, p.Z, Z, p.Z, p.T);
+#endif
   r.X = X;
   r.Y = Y;
   r.Z = Z;
@@ -30,7 +42,12 @@ STL_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
 
 STL_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
   fe X, Y, Z, T;
+#if STL_GE_NOPS == 2
+  fe_mul2(X, p.X, p.T, Y, p.Y, p.Z);
+  fe_mul2(Z, p.Z, p.T, T, p.X, p.Y);
+#else
   fe_mul4(X, p.X, p.T, Y, p.Y, p.Z, Z, p.Z, p.T, T, p.X, p.Y);
+#endif
   r.X = X;
   r.Y = Y;
   r.Z = Z;
@@ -57,7 +74,12 @@ template <bool TO_P2 = false>
 STL_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe XX, YY, ZZ2, A, XpY;
   fe_add(XpY, p.X, p.Y);     // [2]
+#if STL_GE_NOPS == 2
+  fe_sq2(XX, p.X, YY, p.Y);
+  fe_sq2(ZZ2, p.Z, A, XpY);  // A [1]  (2^2 <= 7)
+#else
   fe_sq4(XX, p.X, YY, p.Y, ZZ2, p.Z, A, XpY);  // A [1]  (2^2 <= 7)
+#endif
   fe_add(ZZ2, ZZ2, ZZ2);     // [2]
   fe_add(r.Y, YY, XX);       // [2]
   fe_sub_nc<2>(r.Z, YY, XX); // [3]
@@ -74,7 +96,12 @@ STL_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe A, B, C, D, t, t2;
   fe_sub_nc<2>(t, p.Y, p.X); // [3]
   fe_add(t2, p.Y, p.X);      // [2]
+#if STL_GE_NOPS == 2
+  fe_mul2(A, t, q.YmX, B, t2, q.YpX);  // 3*1, 2*1
+  fe_mul2(C, q.T2d, p.T, D, p.Z, q.Z); // 2*1, 1*1
+#else
   fe_mul4(A, t, q.YmX, B, t2, q.YpX, C, q.T2d, p.T, D, p.Z, q.Z);  // 3*1, 2*1, 2*1, 1*1
+#endif
   fe_add(D, D, D);           // [2]
   fe_sub_nc<2>(r.X, B, A);   // [3]
   fe_add(r.Y, B, A);         // [2]
@@ -88,7 +115,12 @@ STL_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
   fe A, B, C, D, t, t2;
   fe_sub_nc<2>(t, p.Y, p.X); // [3]
   fe_add(t2, p.Y, p.X);      // [2]
+#if STL_GE_NOPS == 2
+  fe_mul2(A, t, q.ymx, B, t2, q.ypx);
+  fe_mul(C, q.xy2d, p.T);
+#else
   fe_mul3(A, t, q.ymx, B, t2, q.ypx, C, q.xy2d, p.T);
+#endif
   fe_add(D, p.Z, p.Z);       // [2]
   fe_sub_nc<2>(r.X, B, A);   // [3]
   fe_add(r.Y, B, A);         // [2]

@@ -371,14 +371,39 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
 
-// Wide-table reader of the main kernel: each lane's two rows (7 x 16 B each)
-// go straight from L2 / the Infinity Cache into its wave's LDS stage by
-// global_load_lds, issued before the position's doublings -- the latency is
-// hidden and no VGPRs are held across the doublings (the kernel runs at
-// 246 of 256).  Stage layout [row][chunk][lane]: conflict-free reads.
+// Wide-table rows in HBM: 7 quads (3 x 9 canonical limbs + a pad word), or,
+// with STL_WIDE_PACKED, 6 quads (3 x 8 words: the canonical values packed
+// like fe_tobytes) -- a 12 KiB LDS stage per wave instead of 14, so three
+// 256-thread workgroups fit in a CU's 160 KiB; unpacked with fe_frombytes.
+#ifdef STL_WIDE_PACKED
+constexpr int kWideQuads = 6;
+#else
+constexpr int kWideQuads = 7;
+#endif
+
+__device__ __forceinline__ void wide_row_to_niels(ge_niels& n, const uint32_t* row) {
+#ifdef STL_WIDE_PACKED
+  fe_frombytes(n.ypx, row);
+  fe_frombytes(n.ymx, row + 8);
+  fe_frombytes(n.xy2d, row + 16);
+#else
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    n.ypx.v[i] = row[i];
+    n.ymx.v[i] = row[9 + i];
+    n.xy2d.v[i] = row[18 + i];
+  }
+#endif
+}
+
+// Wide-table reader of the main kernel: each lane's two rows go straight from
+// L2 / the Infinity Cache into its wave's LDS stage by global_load_lds, issued
+// before the position's doublings -- the latency is hidden and no VGPRs are
+// held across the doublings.  Stage layout [row][chunk][lane]: conflict-free
+// reads.
 struct WideLds {
-  const uint4* gtab;  // 2 * kWideEntries rows of 7 uint4
-  uint4* stage;       // this wave's 2 * 7 * 64 uint4
+  const uint4* gtab;  // 2 * kWideEntries rows of kWideQuads uint4
+  uint4* stage;       // this wave's 2 * kWideQuads * 64 uint4
   uint32_t lane;
   int d[2];
   __device__ void prefetch(int d0, int d1) {
@@ -387,34 +412,31 @@ struct WideLds {
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
       const uint32_t a = (uint32_t)(d[w] < 0 ? -d[w] : d[w]);
-      const uint4* src = gtab + ((size_t)w * kWideEntries + a) * 7;
+      const uint4* src = gtab + ((size_t)w * kWideEntries + a) * kWideQuads;
 #pragma unroll
-      for (int c = 0; c < 7; ++c)
-        __builtin_amdgcn_global_load_lds(src + c, (__attribute__((address_space(3))) void*)(stage + (w * 7 + c) * 64),
+      for (int c = 0; c < kWideQuads; ++c)
+        __builtin_amdgcn_global_load_lds(src + c,
+                                         (__attribute__((address_space(3))) void*)(stage + (w * kWideQuads + c) * 64),
                                          16, 0, 0);
     }
   }
   __device__ void madd(ge_p1p1& t, const ge_p3& acc, int which) const {
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the rows have landed in LDS
-    ge_niels n;
-    uint32_t* w = reinterpret_cast<uint32_t*>(&n);
-    static_assert(sizeof(ge_niels) == 27 * 4, "niels layout");
-    uint32_t row[28];
+    uint32_t row[4 * kWideQuads];
 #pragma unroll
-    for (int c = 0; c < 7; ++c) {
-      const uint4 v = stage[(which * 7 + c) * 64 + lane];
+    for (int c = 0; c < kWideQuads; ++c) {
+      const uint4 v = stage[(which * kWideQuads + c) * 64 + lane];
       row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
     }
-#pragma unroll
-    for (int i = 0; i < 27; ++i) w[i] = row[i];
+    ge_niels n;
+    wide_row_to_niels(n, row);
     ge_niels_cneg(n, d[which] < 0);
     ge_madd(t, acc, n);
   }
 };
 
 // Experiment switch (STL_WIDE_GLOBAL): rows read straight into VGPRs at the
-// madd, no LDS stage (the stage's 57 KB per workgroup caps the kernel at two
-// workgroups = 2 waves/SIMD per CU).
+// madd, no LDS stage.
 struct WideGlobal {
   const uint4* gtab;
   int d[2];
@@ -424,17 +446,15 @@ struct WideGlobal {
   }
   __device__ void madd(ge_p1p1& t, const ge_p3& acc, int which) const {
     const uint32_t a = (uint32_t)(d[which] < 0 ? -d[which] : d[which]);
-    const uint4* src = gtab + ((size_t)which * kWideEntries + a) * 7;
-    ge_niels n;
-    uint32_t* w = reinterpret_cast<uint32_t*>(&n);
-    uint32_t row[28];
+    const uint4* src = gtab + ((size_t)which * kWideEntries + a) * kWideQuads;
+    uint32_t row[4 * kWideQuads];
 #pragma unroll
-    for (int c = 0; c < 7; ++c) {
+    for (int c = 0; c < kWideQuads; ++c) {
       const uint4 v = src[c];
       row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
     }
-#pragma unroll
-    for (int i = 0; i < 27; ++i) w[i] = row[i];
+    ge_niels n;
+    wide_row_to_niels(n, row);
     ge_niels_cneg(n, d[which] < 0);
     ge_madd(t, acc, n);
   }
@@ -459,7 +479,7 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
   WideGlobal wl{wide, {0, 0}};
   (void)lane;
 #else
-  __shared__ uint4 wstage[kBlock / 64][2 * 7 * 64];
+  __shared__ uint4 wstage[kBlock / 64][2 * kWideQuads * 64];
   WideLds wl{wide, wstage[wave], lane, {0, 0}};
 #endif
   for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
@@ -911,9 +931,22 @@ __global__ __launch_bounds__(kBlock) void wide_table_kernel(uint32_t* __restrict
   const int which = r >= kWideEntries ? 1 : 0;
   uint32_t row[28];
   wide_entry(row, which, r - (uint32_t)which * kWideEntries, &kBaseNiels[0][0][0]);
-  uint4* q = reinterpret_cast<uint4*>(out + (size_t)r * kWideRowWords);
+#ifdef STL_WIDE_PACKED
+  uint32_t packed[24];
 #pragma unroll
-  for (int c = 0; c < 7; ++c) q[c] = make_uint4(row[4 * c], row[4 * c + 1], row[4 * c + 2], row[4 * c + 3]);
+  for (int k = 0; k < 3; ++k) {
+    fe f;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) f.v[i] = row[9 * k + i];
+    fe_tobytes(packed + 8 * k, f);  // canonical already: packs the 255 bits
+  }
+  const uint32_t* src = packed;
+#else
+  const uint32_t* src = row;
+#endif
+  uint4* q = reinterpret_cast<uint4*>(out) + (size_t)r * kWideQuads;
+#pragma unroll
+  for (int c = 0; c < kWideQuads; ++c) q[c] = make_uint4(src[4 * c], src[4 * c + 1], src[4 * c + 2], src[4 * c + 3]);
 }
 
 hipError_t launch_wide_table(uint4* out, hipStream_t stream) {
