@@ -294,6 +294,19 @@ struct CallSpan {
   }
 };
 
+// Restores the calling thread's current HIP device on scope exit: the host
+// entry points switch devices internally, and a library call must not leave
+// the caller (stellard, or a PyTorch user of the device API) on another one.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 int current_device_index() {
   int ord = -1;
   if (hipGetDevice(&ord) != hipSuccess) return -1;
@@ -620,6 +633,7 @@ int check_flags(uint32_t flags) {
 int run_batch(const Batch& b, size_t n, uint64_t* gather_ns) {
   if (n == 0) return STL_OK;
   STL_RC(ensure_init());
+  DeviceGuard guard;  // the last shard and the gather run on this thread
   const int g = (int)g_devs.size();
   if (g == 0) return STL_ENODEV;
   // one kernel launch handles up to 2^32-64 signatures per shard
@@ -751,6 +765,7 @@ int stl_init(const stl_config* cfg) {
 
 void stl_shutdown(void) {
   stl_comm_destroy();
+  DeviceGuard guard;
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& d : g_devs) {
     std::lock_guard<std::mutex> dl(d->mu);
@@ -794,6 +809,7 @@ int stl_get_stats(stl_stats* out) {
   out->full_length_lanes = 0;
   for (auto& v : out->phase_ns) v = 0;
   out->phase_chunks = 0;
+  DeviceGuard guard;
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& d : g_devs) {  // device counters: waits for the work queued before the call
     if (!d->counters.p) continue;
@@ -817,6 +833,7 @@ void stl_reset_stats(void) {
   g_st_errors = 0;
   g_st_host_ns = 0;
   g_st_gather_ns = 0;
+  DeviceGuard guard;
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& d : g_devs)
     if (d->counters.p && hipSetDevice(d->ordinal) == hipSuccess) {
@@ -907,6 +924,7 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
   if (mlen > 0xffffffffull) return STL_EINVAL;
   // arbitrary-length message: k = H(R||A||m) mod L on the device, then verify
   STL_RC(ensure_init());
+  DeviceGuard guard;
   Device& d = *g_devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
   STL_TRY(hipSetDevice(d.ordinal));
