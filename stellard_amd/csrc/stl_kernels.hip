@@ -71,12 +71,18 @@ __device__ __forceinline__ void stage_base_table(uint32_t* sB, int tables) {
   __syncthreads();
 }
 
-// Per-lane workspace slot: kSlotQuads uint4 = two 9-entry cached tables,
-// contiguous per lane (one lookup touches 2-3 whole 128-B lines of its own lane).
-__device__ __forceinline__ uint4* lane_slot(uint4* ws) {
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  return ws + (((size_t)blockIdx.x * (kBlock / 64) + wave) * 64 + lane) * kSlotQuads;
+// Per-lane workspace: two 9-entry cached tables per resident lane, split
+// (TableView::split): the entries' 128-B heads, 2 x 9 x 8 quads per lane, in
+// whole aligned lines from the start of the area, then the 16-B tails, 2 x 9
+// quads per lane.  kSlotQuads = 162 quads per lane either way.
+__device__ __forceinline__ void lane_tables(uint4* ws, TableView& t1, TableView& t2) {
+  const size_t lanes = (size_t)gridDim.x * kBlock, gl = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  uint4* head = ws + gl * (2 * 9 * 8);
+  uint4* tails = ws + lanes * (2 * 9 * 8) + gl * (2 * 9);
+  t1 = TableView::split(head, tails);
+  t2 = TableView::split(head + 9 * 8, tails + 9);
 }
+static_assert(kSlotQuads == 2 * 9 * 8 + 2 * 9, "per-lane slot = heads + tails");
 
 template <int NQ, typename T>
 __device__ __forceinline__ void ld_words(T& out, const uint4* q) {
@@ -270,7 +276,7 @@ __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __
   if (nu <= kKeyTables && !wide_keys(nu, cnt)) {  // the shared A-table: j*(-A), j = 0..8, as a lane would build it
     ge_p3 P;
     affine_to_p3(P, negA.X, negA.Y);
-    build_cached_table(TableView{keytabs + (size_t)u * kTableQuadsPerKey, 1}, P);
+    build_cached_table(TableView::contiguous(keytabs + (size_t)u * kTableQuadsPerKey), P);
   }
 }
 
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void key_table_wide_kernel(const uint32_t* 
   }
   ge_cached c;
   ge_p3_to_cached(c, acc);
-  TableView{widetabs + (size_t)u * (kWideKeyEntries * 9), 1}.store((int)j, c);
+  TableView::contiguous(widetabs + (size_t)u * (kWideKeyEntries * 9)).store((int)j, c);
 }
 
 // Phase 1b with the keys already decoded: only R's square-root chain, so the
@@ -472,8 +478,8 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
     uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
     const uint4* __restrict__ keytabs, const uint4* __restrict__ widetabs) {
-  uint4* slot = lane_slot(ws);
-  const TableView tab1{slot, 1}, tab2{slot + kTableQuads, 1};
+  TableView tab1, tab2;
+  lane_tables(ws, tab1, tab2);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
 #ifdef STL_WIDE_GLOBAL
   WideGlobal wl{wide, {0, 0}};
@@ -507,7 +513,8 @@ __global__ __launch_bounds__(kBlock, 2) void verify_fallback_kernel(
     uint64_t* __restrict__ bitmap, uint4* __restrict__ ws, unsigned long long* __restrict__ ctr) {
   __shared__ uint32_t sB[kBaseTableWords];
   stage_base_table(sB, 1);
-  const TableView tab{lane_slot(ws), 1};
+  TableView tab, unused;
+  lane_tables(ws, tab, unused);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
     const uint32_t wbase = tile + wave * 64;
@@ -872,7 +879,8 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
                                                       uint4* __restrict__ ws) {
   __shared__ uint32_t sB[kBaseTableWords];
   stage_base_table(sB, 1);
-  const TableView tv{lane_slot(ws), 1};
+  TableView tv, unused;
+  lane_tables(ws, tv, unused);
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     const uint32_t i = base + threadIdx.x;
     const bool live = i < n;

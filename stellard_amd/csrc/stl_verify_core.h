@@ -82,14 +82,21 @@ STL_HD bool verify_prechecks(const uint32_t R[8], const uint32_t S[8], const uin
 
 constexpr uint32_t kTableQuadsPerKey = 9 * 9;  // a 9-entry cached table, 9 x uint4 per entry
 
-// Per-lane table of cached multiples e*(-A), e = 0..8, 9 x uint4 per entry.
-// stride = distance (in uint4) between consecutive quads of one entry; the
-// kernel keeps each lane's 1296-byte table contiguous (stride 1).
+// Table of cached multiples e*P (9 x uint4 = 144 B per entry).  Quads 0-7 of
+// entry e are at main[e * estride + q], quad 8 at tail[e * tstride]:
+//   contiguous  one 1,296-B block, entry after entry (estride = tstride = 9):
+//               the shared per-key tables of STL_DEDUP_KEYS;
+//   split       per-lane tables: the 128-B heads in an array of whole lines
+//               (estride 8) and the 16-B tails packed apart (tstride 1), so a
+//               lookup reads one aligned line plus a tail from the lane's
+//               small, hot tail block instead of two lines per entry.
 struct TableView {
-  uint4* base;
-  int stride;
+  uint4* main;
+  uint4* tail;
+  int estride, tstride;
+  static STL_HD TableView contiguous(uint4* base) { return TableView{base, base + 8, 9, 9}; }
+  static STL_HD TableView split(uint4* head, uint4* tails) { return TableView{head, tails, 8, 1}; }
   STL_HD void store(int e, const ge_cached& c) const {
-    const uint32_t* w = &c.YpX.v[0];
     uint32_t buf[36];
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -98,16 +105,16 @@ struct TableView {
       buf[18 + i] = c.Z.v[i];
       buf[27 + i] = c.T2d.v[i];
     }
-    (void)w;
 #pragma unroll
-    for (int q = 0; q < 9; ++q)
-      base[(e * 9 + q) * stride] = make_uint4(buf[4 * q], buf[4 * q + 1], buf[4 * q + 2], buf[4 * q + 3]);
+    for (int q = 0; q < 8; ++q)
+      main[e * estride + q] = make_uint4(buf[4 * q], buf[4 * q + 1], buf[4 * q + 2], buf[4 * q + 3]);
+    tail[e * tstride] = make_uint4(buf[32], buf[33], buf[34], buf[35]);
   }
   STL_HD void load(int e, ge_cached& c) const {
     uint32_t buf[36];
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
-      const uint4 v = base[(e * 9 + q) * stride];
+      const uint4 v = q < 8 ? main[e * estride + q] : tail[e * tstride];
       buf[4 * q] = v.x;
       buf[4 * q + 1] = v.y;
       buf[4 * q + 2] = v.z;
@@ -552,8 +559,8 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
   kwide = kwide && keyed;
   const bool a_flip = keyed && (p.tops & kHalfCNeg) != 0;  // key table holds j*(-A); P1 = +A when c < 0
   const TableView t1 =
-      kwide ? TableView{const_cast<uint4*>(widetabs) + (size_t)p.pad * (kWideKeyEntries * 9), 1}
-            : keyed ? TableView{const_cast<uint4*>(keytabs) + (size_t)p.pad * kTableQuadsPerKey, 1} : tab1;
+      kwide ? TableView::contiguous(const_cast<uint4*>(widetabs) + (size_t)p.pad * (kWideKeyEntries * 9))
+            : keyed ? TableView::contiguous(const_cast<uint4*>(keytabs) + (size_t)p.pad * kTableQuadsPerKey) : tab1;
   {
     ge_p3 P;
     if (!keyed) {
@@ -624,8 +631,17 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     // of independent work per wave): their latency (L2 / Infinity Cache) is
     // hidden instead of stalling the adds.
     ge_cached ca, cq;
-#ifndef STL_NO_TABLE_PREFETCH
-    if (cadd) t1.load(dc < 0 ? -dc : dc, ca);
+#if defined(STL_EXP_ENTRY0)
+    // timing experiment only (wrong results): every lookup reads entry 0 of
+    // its table (cache-resident) -- the memory-side cost of the lookups
+    if (cadd) t1.load(0, ca);
+    tab2.load(0, cq);
+#elif !defined(STL_NO_TABLE_PREFETCH)
+    // Unconditional loads (entry 0 where a wide-key position skips the A-add):
+    // a load under `if (cadd)` made the compiler merge its registers at the
+    // end of the branch, i.e. wait for the load there -- before the doublings
+    // it is meant to overlap.
+    t1.load(cadd ? (dc < 0 ? -dc : dc) : 0, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
 #endif
     if (bpos) wide.prefetch(de0, de1);

@@ -81,7 +81,7 @@ extern "C" {
 uint64_t hostemu_verify_batch_mode(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
                                    uint8_t* bitmap, uint32_t policy, int mode, uint64_t* fallbacks) {
   std::vector<uint4> table(2 * 81);
-  stl::TableView t1{table.data(), 1}, t2{table.data() + 81, 1};
+  const stl::TableView t1 = stl::TableView::contiguous(table.data()), t2 = stl::TableView::contiguous(table.data() + 81);
   const uint32_t* btab = &stl::kBaseNielsHost[0][0][0];
   std::memset(bitmap, 0, (n + 7) / 8);
   uint64_t fb = 0;
