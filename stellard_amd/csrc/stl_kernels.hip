@@ -441,8 +441,9 @@ struct WideLds {
   }
 };
 
-// Experiment switch (STL_WIDE_GLOBAL): rows read straight into VGPRs at the
-// madd, no LDS stage.
+// Wide rows read straight into VGPRs at the madd (the default, since the
+// per-lane table tails take the LDS; with STL_TAILS_GLOBAL the rows are staged
+// in LDS by WideLds instead).
 struct WideGlobal {
   const uint4* gtab;
   int d[2];
@@ -480,8 +481,19 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const uint4* __restrict__ keytabs, const uint4* __restrict__ widetabs) {
   TableView tab1, tab2;
   lane_tables(ws, tab1, tab2);
+#ifndef STL_TAILS_GLOBAL
+  // The tables' 16-B tails live in LDS, [table*9 + entry][lane] (conflict-
+  // free; 72 KiB per workgroup, two workgroups per CU): a lookup reads one
+  // aligned HBM line (its head) and one LDS quad.  LDS then has no room for
+  // the wide-row stage, so wide rows are read into VGPRs at their madd.
+  // Same-box A/B: main kernel -4.1 %.
+  __shared__ uint4 tails[18][kBlock];
+  tab1.tail = &tails[0][threadIdx.x];
+  tab2.tail = &tails[9][threadIdx.x];
+  tab1.tstride = tab2.tstride = kBlock;
+#endif
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-#ifdef STL_WIDE_GLOBAL
+#if defined(STL_WIDE_GLOBAL) || !defined(STL_TAILS_GLOBAL)
   WideGlobal wl{wide, {0, 0}};
   (void)lane;
 #else

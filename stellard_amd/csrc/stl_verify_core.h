@@ -95,7 +95,9 @@ struct TableView {
   uint4* tail;
   int estride, tstride;
   static STL_HD TableView contiguous(uint4* base) { return TableView{base, base + 8, 9, 9}; }
-  static STL_HD TableView split(uint4* head, uint4* tails) { return TableView{head, tails, 8, 1}; }
+  static STL_HD TableView split(uint4* head, uint4* tails, int tstride = 1) {
+    return TableView{head, tails, 8, tstride};
+  }
   STL_HD void store(int e, const ge_cached& c) const {
     uint32_t buf[36];
 #pragma unroll
