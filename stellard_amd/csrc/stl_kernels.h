@@ -8,8 +8,11 @@ namespace stl {
 
 constexpr uint32_t kBlock = 256;          // threads per workgroup (4 waves)
 constexpr uint32_t kTableQuads = 9 * 9;   // 9 cached entries x 9 uint4 (144 B each)
-constexpr uint32_t kSlotQuads = 2 * kTableQuads;  // per-lane slot: two tables
-// workspace bytes per resident workgroup: 256 lanes x 162 x 16 B = 648 KiB
+// per-lane slot: two split tables (stl_kernels.hip lane_tables): 2 x 8 heads
+// of 8 quads (entry 0, the identity, shares one line) + 2 x 9 tail quads
+constexpr uint32_t kHeadQuads = 2 * 8 * 8;
+constexpr uint32_t kSlotQuads = kHeadQuads + 2 * 9;
+// workspace bytes per resident workgroup: 256 lanes x 146 x 16 B = 584 KiB
 constexpr size_t kWsBytesPerBlock = (size_t)kBlock * kSlotQuads * 16;
 // verify phase-1 state (HalfState, 224 B) is produced and consumed in chunks
 // of kPreChunk signatures (a multiple of 64, so chunks start on bitmap words),

@@ -72,17 +72,60 @@ __device__ __forceinline__ void stage_base_table(uint32_t* sB, int tables) {
 }
 
 // Per-lane workspace: two 9-entry cached tables per resident lane, split
-// (TableView::split): the entries' 128-B heads, 2 x 9 x 8 quads per lane, in
-// whole aligned lines from the start of the area, then the 16-B tails, 2 x 9
-// quads per lane.  kSlotQuads = 162 quads per lane either way.
+// (TableView::split): the 128-B heads of entries 1-8, 2 x 8 x 8 quads per
+// lane, in whole aligned lines from the start of the area, then the 16-B
+// tails, 2 x 9 quads per lane (the main kernel keeps its tails in LDS).  Entry
+// 0 is the identity; its head is kIdentityHead, shared by every lane.
+__device__ __attribute__((aligned(128))) const uint4 kIdentityHead[8] = {
+    {1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 1u, 0u, 0u}, {0u, 0u, 0u, 0u},
+    {0u, 0u, 1u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};  // YpX = YmX = Z = 1, T2d = 0
 __device__ __forceinline__ void lane_tables(uint4* ws, TableView& t1, TableView& t2) {
-  const size_t lanes = (size_t)gridDim.x * kBlock, gl = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  uint4* head = ws + gl * (2 * 9 * 8);
-  uint4* tails = ws + lanes * (2 * 9 * 8) + gl * (2 * 9);
-  t1 = TableView::split(head, tails);
-  t2 = TableView::split(head + 9 * 8, tails + 9);
+  const size_t lanes = (size_t)gridDim.x * kBlock;
+#ifdef STL_EXP_HALF_FOOTPRINT
+  // timing experiment only (lanes 2i, 2i+1 share a slot: wrong results): the
+  // per-lane tables' footprint halved, below the 256 MB Infinity Cache
+  const size_t gl = ((size_t)blockIdx.x * kBlock + threadIdx.x) >> 1;
+#else
+  const size_t gl = (size_t)blockIdx.x * kBlock + threadIdx.x;
+#endif
+  uint4* head = ws + gl * kHeadQuads;
+  uint4* tails = ws + lanes * kHeadQuads + gl * (2 * 9);
+  t1 = TableView::split(head, tails, kIdentityHead);
+  t2 = TableView::split(head + kHeadQuads / 2, tails + 9, kIdentityHead);
 }
-static_assert(kSlotQuads == 2 * 9 * 8 + 2 * 9, "per-lane slot = heads + tails");
+static_assert(kSlotQuads >= kHeadQuads + 2 * 9, "per-lane slot = heads + tails");
+
+// Phase-1 state (HalfState) is written once and read once: with STL_NT_STATE
+// it moves with non-temporal loads / stores so it does not displace the
+// per-lane tables in the Infinity Cache.
+typedef unsigned int stl_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_state(uint4* p, uint4 v) {
+#ifdef STL_NT_STATE
+  stl_u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<stl_u32x4*>(p));
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ uint4 ld_state(const uint4* p) {
+#ifdef STL_NT_STATE
+  const stl_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const stl_u32x4*>(p));
+  return make_uint4(x.x, x.y, x.z, x.w);
+#else
+  return *p;
+#endif
+}
+
+template <int NQ, typename T>
+__device__ __forceinline__ void ld_state_words(T& out, const uint4* q) {
+  static_assert(sizeof(T) == NQ * 16, "size");
+  uint32_t* w = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const uint4 v = ld_state(q + i);
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+}
 
 template <int NQ, typename T>
 __device__ __forceinline__ void ld_words(T& out, const uint4* q) {
@@ -138,7 +181,7 @@ __global__ __launch_bounds__(kBlock, STL_SCALAR_WAVES_PER_SIMD) void verify_scal
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
   uint4* q = pre + (size_t)t * 14;
 #pragma unroll
-  for (int i = 0; i < kHalfScalarQuads; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  for (int i = 0; i < kHalfScalarQuads; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
 }
 
 // Phase 1b: pre-checks, decompression of A and R, signed P1 / P2, final
@@ -164,9 +207,9 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_point_k
   verify_phase1_points(h, R, S, A, policy & 1u);
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
   if (live) {
-    q[kHalfTopsWord / 4] = make_uint4(w[8], w[9], w[10], w[11]);
+    st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
 #pragma unroll
-    for (int i = kHalfScalarQuads; i < 14; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+    for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
   }
   const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
@@ -369,9 +412,9 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   if (wide_keys(nu, cnt)) h.tops |= kHalfKeyedWide;
   if (live) {
     q[4] = make_uint4(w[16], w[17], w[18], w[19]);
-    q[kHalfTopsWord / 4] = make_uint4(w[8], w[9], w[10], w[11]);
+    st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
 #pragma unroll
-    for (int i = kHalfScalarQuads; i < 14; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+    for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
   }
   const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
@@ -504,7 +547,7 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const uint32_t t = tile + threadIdx.x;
     const bool live = t < cnt;
     HalfState h;
-    ld_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
+    ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
     const bool ok = verify_phase2_half(h, tab1, tab2, wl, keytabs, widetabs) && live;
     const uint64_t word = __ballot(ok);
     const uint32_t wbase = tile + wave * 64;

@@ -86,17 +86,24 @@ constexpr uint32_t kTableQuadsPerKey = 9 * 9;  // a 9-entry cached table, 9 x ui
 // entry e are at main[e * estride + q], quad 8 at tail[e * tstride]:
 //   contiguous  one 1,296-B block, entry after entry (estride = tstride = 9):
 //               the shared per-key tables of STL_DEDUP_KEYS;
-//   split       per-lane tables: the 128-B heads in an array of whole lines
-//               (estride 8) and the 16-B tails packed apart (tstride 1), so a
-//               lookup reads one aligned line plus a tail from the lane's
-//               small, hot tail block instead of two lines per entry.
+//   split       per-lane tables: the 128-B heads of entries 1-8 in an array
+//               of whole lines (estride 8; entry 0's head is a shared
+//               identity line) and the 16-B tails apart (in LDS in the main
+//               kernel), so a lookup reads one aligned line.
 struct TableView {
   uint4* main;
   uint4* tail;
   int estride, tstride;
-  static STL_HD TableView contiguous(uint4* base) { return TableView{base, base + 8, 9, 9}; }
-  static STL_HD TableView split(uint4* head, uint4* tails, int tstride = 1) {
-    return TableView{head, tails, 8, tstride};
+  // split tables do not store entry 0 (the identity): its head is this one
+  // shared line (L2-resident), so the per-lane heads are 8 lines per table
+  const uint4* id;
+  static STL_HD TableView contiguous(uint4* base) { return TableView{base, base + 8, 9, 9, nullptr}; }
+  static STL_HD TableView split(uint4* head, uint4* tails, const uint4* id_head, int tstride = 1) {
+    return TableView{head, tails, 8, tstride, id_head};
+  }
+  STL_HD const uint4* head(int e) const {
+    if (id) return e == 0 ? id : main + (e - 1) * estride;
+    return main + e * estride;
   }
   STL_HD void store(int e, const ge_cached& c) const {
     uint32_t buf[36];
@@ -107,16 +114,19 @@ struct TableView {
       buf[18 + i] = c.Z.v[i];
       buf[27 + i] = c.T2d.v[i];
     }
+    if (!(id && e == 0)) {
+      uint4* h = const_cast<uint4*>(head(e));
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      main[e * estride + q] = make_uint4(buf[4 * q], buf[4 * q + 1], buf[4 * q + 2], buf[4 * q + 3]);
+      for (int q = 0; q < 8; ++q) h[q] = make_uint4(buf[4 * q], buf[4 * q + 1], buf[4 * q + 2], buf[4 * q + 3]);
+    }
     tail[e * tstride] = make_uint4(buf[32], buf[33], buf[34], buf[35]);
   }
   STL_HD void load(int e, ge_cached& c) const {
     uint32_t buf[36];
+    const uint4* h = head(e);
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
-      const uint4 v = q < 8 ? main[e * estride + q] : tail[e * tstride];
+      const uint4 v = q < 8 ? h[q] : tail[e * tstride];
       buf[4 * q] = v.x;
       buf[4 * q + 1] = v.y;
       buf[4 * q + 2] = v.z;
