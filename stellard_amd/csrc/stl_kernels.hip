@@ -82,6 +82,7 @@ __device__ __attribute__((aligned(128))) const uint4 kIdentityHead[8] = {
 __device__ __forceinline__ void lane_tables(uint4* ws, TableView& t1, TableView& t2) {
   const size_t lanes = (size_t)gridDim.x * kBlock;
 #ifdef STL_EXP_HALF_FOOTPRINT
+#warning "STL_EXP_HALF_FOOTPRINT is a timing experiment: verification results are wrong"
   // timing experiment only (lanes 2i, 2i+1 share a slot: wrong results): the
   // per-lane tables' footprint halved, below the 256 MB Infinity Cache
   const size_t gl = ((size_t)blockIdx.x * kBlock + threadIdx.x) >> 1;

@@ -644,6 +644,7 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     // hidden instead of stalling the adds.
     ge_cached ca, cq;
 #if defined(STL_EXP_ENTRY0)
+#warning "STL_EXP_ENTRY0 is a timing experiment: verification results are wrong"
     // timing experiment only (wrong results): every lookup reads entry 0 of
     // its table (cache-resident) -- the memory-side cost of the lookups
     if (cadd) t1.load(0, ca);
