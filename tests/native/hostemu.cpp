@@ -113,6 +113,55 @@ uint64_t hostemu_verify_batch_mode(const uint8_t* sig, const uint8_t* msg, const
   return g_bound_viol.load();
 }
 
+// The product path (mode 0) with the kernels' split table layout
+// (TableView::split): heads of entries 1-8 in one array, entry 0's head one
+// shared identity line, tails in a separate array at stride `tstride` quads
+// (the main kernel's LDS layout [table*9 + entry][lane] has stride 256).
+uint64_t hostemu_verify_batch_split(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
+                                    uint8_t* bitmap, uint32_t policy, int tstride) {
+  std::vector<uint4> heads(2 * 8 * 8), tails((size_t)18 * tstride), id(9);
+  stl::ge_cached idc;
+  stl::ge_cached_0(idc);
+  stl::TableView::contiguous(id.data()).store(0, idc);  // identity entry: its 8-quad head
+  const stl::TableView t1 = stl::TableView::split(heads.data(), tails.data(), id.data(), tstride),
+                       t2 = stl::TableView::split(heads.data() + 64, tails.data() + (size_t)9 * tstride, id.data(),
+                                                  tstride);
+  std::vector<uint4> full(81);
+  const stl::TableView tf = stl::TableView::contiguous(full.data());
+  const uint32_t* btab = &stl::kBaseNielsHost[0][0][0];
+  std::memset(bitmap, 0, (n + 7) / 8);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t R[8], S[8], A[8], M[8], h[16], k[8];
+    load8(R, sig + 64 * i);
+    load8(S, sig + 64 * i + 32);
+    load8(A, pk + 32 * i);
+    load8(M, msg + 32 * i);
+    stl::sha512_hram32(h, R, A, M);
+    stl::sc_reduce64(k, h);
+    stl::HalfState hs;
+    stl::verify_phase1_half(hs, R, S, A, k, policy);
+    bool ok;
+    if (hs.tops & stl::kHalfFallback) {
+      ok = stl::verify_full_with_k(R, S, A, k, policy, tf, btab);
+    } else {
+      stl::WideHost wide{wide_tables(), {0, 0}};
+      ok = stl::verify_phase2_half(hs, t1, t2, wide);
+    }
+    if (ok) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  return g_bound_viol.load();
+}
+
+// Words of the identity entry's head as the split tables expect it (the
+// device constant kIdentityHead must equal these 32 words).
+void hostemu_identity_head(uint32_t out[32]) {
+  std::vector<uint4> id(9);
+  stl::ge_cached idc;
+  stl::ge_cached_0(idc);
+  stl::TableView::contiguous(id.data()).store(0, idc);
+  std::memcpy(out, id.data(), 32 * 4);
+}
+
 uint64_t hostemu_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
                               uint8_t* bitmap, uint32_t policy) {
   return hostemu_verify_batch_mode(sig, msg, pk, n, bitmap, policy, 0, nullptr);

@@ -252,6 +252,9 @@ def load_hostemu():
     lib.hostemu_bound_checks.restype = ctypes.c_uint64
     lib.hostemu_verify_batch_mode.restype = ctypes.c_uint64
     lib.hostemu_verify_batch_mode.argtypes = [V, V, V, ctypes.c_size_t, V, ctypes.c_uint32, ctypes.c_int, V]
+    lib.hostemu_verify_batch_split.restype = ctypes.c_uint64
+    lib.hostemu_verify_batch_split.argtypes = [V, V, V, ctypes.c_size_t, V, ctypes.c_uint32, ctypes.c_int]
+    lib.hostemu_identity_head.argtypes = [V]
     lib.hostemu_lattice.restype = ctypes.c_int
     lib.hostemu_lattice.argtypes = [V, V, V, V]
     lib.hostemu_sc_mul_signed.argtypes = [V, ctypes.c_int, V, V]

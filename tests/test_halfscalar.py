@@ -170,6 +170,35 @@ def test_paths_vs_golden(emu, golden, policy, key, mode):
         assert fb == 0
 
 
+@pytest.mark.parametrize("tstride", [1, 256])
+@pytest.mark.parametrize("policy,key", [(0, "expected_sodium_1_0_18"), (1, "expected_stellard_1_0_0_unpinned")])
+def test_split_table_layout_vs_golden(emu, golden, policy, key, tstride):
+    """The kernels' split per-lane tables (TableView::split: 128-B heads of
+    entries 1-8, a shared identity head, tails at stride 1 or the main kernel's
+    LDS stride 256) give the golden bits, like the contiguous layout."""
+    sig, msg, pk = golden["sig"], golden["msg"], golden["pk"]
+    n = sig.shape[0]
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    B = lambda a: np.ascontiguousarray(a).ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    viol = emu.hostemu_verify_batch_split(B(sig), B(msg), B(pk), n, B(bm), policy, tstride)
+    assert viol == 0
+    got = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    assert np.array_equal(got, golden[key].astype(bool))
+
+
+def test_identity_head_constant(emu):
+    """kIdentityHead (stl_kernels.hip) holds the identity entry's head as the
+    split tables store it: YpX = YmX = Z = 1, T2d = 0, 9 limbs each."""
+    import re
+    out = (ctypes.c_uint32 * 32)()
+    emu.hostemu_identity_head(out)
+    src = open(__file__.replace("tests/test_halfscalar.py", "stellard_amd/csrc/stl_kernels.hip")).read()
+    body = src[src.index("kIdentityHead[8] = {"):]
+    body = body[:body.index("};")]
+    words = [int(x) for x in re.findall(r"(\d+)u", body)]
+    assert words == list(out)
+
+
 @pytest.mark.parametrize("policy", [0, 1])
 def test_half_vs_full_vs_oracle_mutated(emu, oracle, policy):
     rng = np.random.default_rng(1000 + policy)
