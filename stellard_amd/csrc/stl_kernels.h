@@ -7,7 +7,6 @@
 namespace stl {
 
 constexpr uint32_t kBlock = 256;          // threads per workgroup (4 waves)
-constexpr uint32_t kTableQuads = 9 * 9;   // 9 cached entries x 9 uint4 (144 B each)
 // per-lane slot: two split tables (stl_kernels.hip lane_tables): 2 x 8 heads
 // of 8 quads (entry 0, the identity, shares one line) + 2 x 9 tail quads
 constexpr uint32_t kHeadQuads = 2 * 8 * 8;

@@ -11,11 +11,12 @@
 //
 // Scalar multiplication: joint fixed-window (signed radix 16) Straus with
 // shared doublings -- uniform control flow across the wave (no per-lane
-// sliding-window branches).  [k](-A) uses a 9-entry per-lane table of cached
-// multiples of -A held in a lane-interleaved HBM/L2 workspace; [S]B uses the
-// constant affine table of j*B.  The result is the same group element as
-// libsodium's sliding-window ge25519_double_scalarmult_vartime, so encode()
-// matches byte-for-byte.
+// sliding-window branches).  Variable points use 9-entry per-lane tables of
+// cached multiples (TableView: HBM heads, LDS or HBM tails); [S]B / [e]B use
+// constant affine tables of j*B.  The full-length check gives the same group
+// element as libsodium's sliding-window ge25519_double_scalarmult_vartime, so
+// encode() matches byte-for-byte; the half-size check is exact by the argument
+// before verify_phase2_half.
 #pragma once
 #include "stl_ge25519.h"
 #include "stl_sc25519.h"
