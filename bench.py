@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="launcher/control-plane rehearsal on CPUs, no GPU")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the configs[2] / configs[4] legs reported under extra_configs")
     return ap.parse_args()
 
 
@@ -184,6 +186,114 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def extra_configs(world, rank, dist, V, torch, dev, stream, sig, msgs, pk, gather_into):
+    """The other multi-GPU configs of BASELINE.json, measured after the timed
+    bench steps and reported under ``extra_configs`` (not ``value``):
+      configs[2]  67,108,864 signatures over the N ranks (64M / N per rank: the
+                  rank's bench batch tiled, so the work is real verification of
+                  valid signatures), one stl_ed25519_verify_batch_device call
+                  per rank (2^20-signature chunks inside) + the RCCL bitmap
+                  gather to rank 0, timed barrier-to-barrier;
+      configs[4]  ledger replay: 2^20 transactions per rank (weak scaling),
+                  signing preimages log-uniform in [113 B, 4 KB] (random bytes of
+                  those lengths; 1,000 signers), SHA512Half + verify on the
+                  device (the device-resident checkSign), without and with
+                  STL_DEDUP_KEYS, + the bitmap gather.
+    Each rank checks its own inputs first; the collectives run only when every
+    rank succeeded, so one rank's failure cannot leave another in a gather."""
+    import numpy as np  # noqa: F811
+    out, err = {}, None
+    n = sig.shape[0]
+    try:
+        n3 = (1 << 26) // world
+        reps3 = -(-n3 // n)
+        sig3 = sig.repeat(reps3, 1)[:n3].contiguous()
+        msg3 = msgs.repeat(reps3, 1)[:n3].contiguous()
+        pk3 = pk.repeat(reps3, 1)[:n3].contiguous()
+        w3 = torch.empty((n3 + 63) // 64, dtype=torch.int64, device=dev)
+        V.verify_batch_device(sig3, msg3, pk3, out_words=w3, stream=stream)  # warm + check
+        torch.cuda.synchronize()
+        ok3 = bool(V.words_to_bool(w3, n3).all())
+        rng = np.random.default_rng(0x5EED0005 + rank)
+        n5 = 1 << 20
+        lens = np.exp(rng.uniform(np.log(113), np.log(4096), n5)).astype(np.int32)
+        offs = np.zeros(n5, np.int64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.int64)
+        total = int(offs[-1] + lens[-1])
+        g = torch.Generator(device=dev)
+        g.manual_seed(0x5EED0005 + rank)
+        pre = torch.randint(0, 256, (total + 16,), dtype=torch.uint8, device=dev, generator=g)
+        d_off = torch.from_numpy(offs).to(dev)
+        d_len = torch.from_numpy(lens).to(dev)
+        signers = torch.randint(0, 256, (1000, 32), dtype=torch.uint8, device=dev, generator=g)
+        seeds5 = signers[torch.arange(n5, device=dev) % 1000].contiguous()
+        m5 = V.tx_hash_batch_device(pre, d_off, d_len, stream=stream)
+        pk5, sig5 = V.sign_batch_device(seeds5, m5)
+        w5 = torch.empty((n5 + 63) // 64, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+
+        def leg5(flags):
+            V.tx_hash_batch_device(pre, d_off, d_len, out_msg=m5, stream=stream)
+            V.verify_batch_device(sig5, m5, pk5, out_words=w5, policy=flags, stream=stream)
+
+        leg5(0)
+        torch.cuda.synchronize()
+        ok5 = bool(V.words_to_bool(w5, n5).all())
+    except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench line
+        err = f"rank {rank}: {e!r}"
+    errs = [err]
+    if world > 1:
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+    if any(errs):
+        return {"error": next(e for e in errs if e)}
+
+    def timed(fn, words, wpr, reps):
+        full = torch.empty(wpr * world, dtype=torch.int64, device=dev) if world > 1 and rank == 0 else None
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            fn()
+            if world > 1:
+                gather_into(words, full)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            ts.append(time.perf_counter() - t0)
+        t = torch.tensor([float(np.median(ts))], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gathered = None
+        if world > 1 and rank == 0:
+            gathered = bool(V.words_to_bool(full, wpr * 64 * world).all())
+        return float(t[0]), gathered
+
+    dt3, g3 = timed(lambda: V.verify_batch_device(sig3, msg3, pk3, out_words=w3, stream=stream), w3, w3.shape[0], 3)
+    dt5, g5 = timed(lambda: leg5(0), w5, w5.shape[0], 5)
+    dt5d, _ = timed(lambda: leg5(V.DEDUP_KEYS), w5, w5.shape[0], 5)
+    oks = [ok3 and ok5]
+    if world > 1:
+        oks = [None] * world
+        dist.all_gather_object(oks, ok3 and ok5)
+    out["config3_64M"] = {
+        "signatures_total": n3 * world, "signatures_per_rank": n3, "verifies_per_s": n3 * world / dt3,
+        "ms": dt3 * 1e3, "median_of": 3, "all_accepted_every_rank": all(oks), "gathered_all_accepted": g3,
+        "data": "each rank's bench batch (GPU-signed, distinct keys) tiled to 64M/N signatures",
+        "timing": "barrier, one verify call per rank (+ RCCL gather to rank 0 at N > 1), sync, barrier; max over ranks"}
+    out["config5_ledger_replay"] = {
+        "transactions_per_rank": n5, "transactions_total": n5 * world, "preimage_bytes_per_rank": total,
+        "tx_per_s": n5 * world / dt5, "ms": dt5 * 1e3, "tx_per_s_dedup_keys": n5 * world / dt5d,
+        "ms_dedup_keys": dt5d * 1e3, "median_of": 5, "gathered_all_accepted": g5,
+        "data": "per rank 2^20 preimages of random bytes, lengths log-uniform in [113, 4096], 1,000 signers, "
+                "GPU-signed over their SHA512Half",
+        "timing": "barrier, SHA512Half + verify (device-resident checkSign) per rank (+ RCCL gather at N > 1), "
+                  "sync, barrier; max over ranks"}
+    return out
+
+
 def gpu_run(args, world, rank, local):
     import torch
     dist = control_plane(world, rank)
@@ -236,14 +346,17 @@ def gpu_run(args, world, rank, local):
     full_words = torch.empty(wpr * world, dtype=torch.int64, device=dev) if world > 1 and rank == 0 else None
     stream = torch.cuda.current_stream()
 
-    def gather():
+    def gather_into(w, full):
         if nccl_group is None:
-            V.bitmap_gather_device(words, full_words, root=0, stream=stream)
+            V.bitmap_gather_device(w, full, root=0, stream=stream)
         else:
-            parts = [torch.empty_like(words) for _ in range(world)]
-            dist.all_gather(parts, words, group=nccl_group)
+            parts = [torch.empty_like(w) for _ in range(world)]
+            dist.all_gather(parts, w, group=nccl_group)
             if rank == 0:
-                torch.cat(parts, out=full_words)
+                torch.cat(parts, out=full)
+
+    def gather():
+        gather_into(words, full_words)
 
     def step():
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
@@ -285,6 +398,12 @@ def gpu_run(args, world, rank, local):
 
     st = V.get_stats()  # device counters over the K timed launches (after the sync above)
     V.set_phase_timing(False)
+    extra = None
+    if not args.no_extra:
+        try:
+            extra = extra_configs(world, rank, dist, V, torch, dev, stream, sig, msgs, pk, gather_into)
+        except Exception as e:  # noqa: BLE001 - the extra legs must not cost the bench line
+            extra = {"error": f"rank {rank}: {e!r}"}
     chunks = max(1, st["phase_chunks"])
     phase_ms = {k: v / chunks / 1e6 for k, v in st["phase_ns"].items()}  # average per launch (one chunk each)
     if rank == 0:
@@ -346,6 +465,7 @@ def gpu_run(args, world, rank, local):
             "stats": {"source": "stl_get_stats over the timed launches (rank 0)",
                       "accepted": st["accepted"], "full_length_lanes": st["full_length_lanes"],
                       "verifies": n * args.steps},
+            "extra_configs": extra,
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

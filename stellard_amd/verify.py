@@ -280,6 +280,27 @@ def verify_batch_device(sig, msg, pk, out_words=None, policy=POLICY_SODIUM_1_0_1
     return out_words
 
 
+def tx_hash_batch_device(preimages, offsets, lengths, out_msg=None, stream=None):
+    """SHA512Half of signing preimages already in HBM (uint8 / int64 / int32
+    CUDA tensors; getSigningHash, SerializedObject.cpp:444-450) -> (n,32) uint8
+    signing hashes, asynchronously on ``stream``; with verify_batch_device this
+    is the device-resident checkSign (stl_tx_verify_batch)."""
+    import torch
+    n = offsets.shape[0]
+    if out_msg is None:
+        out_msg = torch.empty((n, 32), dtype=torch.uint8, device=preimages.device)
+    for t in (preimages, offsets, lengths, out_msg):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("device entry point needs contiguous CUDA tensors")
+    if offsets.dtype != torch.int64 or lengths.dtype != torch.int32:
+        raise ValueError("offsets must be int64 and lengths int32")
+    N.check(N.load().stl_tx_hash_batch_device(
+        ctypes.c_void_p(preimages.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+        ctypes.c_void_p(lengths.data_ptr()), n, ctypes.c_void_p(out_msg.data_ptr()), _stream_ptr(stream)),
+        "stl_tx_hash_batch_device")
+    return out_msg
+
+
 def tx_blob_prepare_device(blobs, offsets, lengths, tx_ids=True, stream=None, kind=None):
     """Serialized transactions already in HBM (uint8 / int64 / int32 CUDA
     tensors) -> dict of msg (n,32), sig (n,64), pk (n,32), status (n,) and
