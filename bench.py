@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="launcher/control-plane rehearsal on CPUs, no GPU")
+    ap.add_argument("--gather", choices=("rccl", "gloo"), default="rccl",
+                    help="bitmap gather at N > 1: libstl's RCCL (the product), or gloo through host memory -- a "
+                         "rehearsal of the multi-rank flow with every rank on the visible GPU(s), e.g. 2 ranks on "
+                         "a 1-GPU box (RCCL refuses two ranks on one device)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the configs[2] / configs[4] legs reported under extra_configs")
     return ap.parse_args()
@@ -297,7 +301,8 @@ def extra_configs(world, rank, dist, V, torch, dev, stream, sig, msgs, pk, gathe
 def gpu_run(args, world, rank, local):
     import torch
     dist = control_plane(world, rank)
-    torch.cuda.set_device(local)
+    rehearsal = world > 1 and args.gather == "gloo"
+    torch.cuda.set_device(local % torch.cuda.device_count() if rehearsal else local)
     from stellard_amd import verify as V
 
     V.init(device_count=1, first_device=torch.cuda.current_device())
@@ -307,7 +312,9 @@ def gpu_run(args, world, rank, local):
     assert (lo, hi) == (rank * n, (rank + 1) * n) or n % 64, "per-rank shards are whole ballot words"
     gather_via = None
     nccl_group = None
-    if world > 1:
+    if rehearsal:
+        gather_via = "gloo through host memory (rehearsal of the multi-rank flow, not the RCCL product path)"
+    elif world > 1:
         # rank 0 makes the RCCL unique id; gloo carries it to every rank.  If
         # libstl's communicator cannot be built on some rank, every rank falls
         # back to torch.distributed's RCCL (backend "nccl") for the gather and
@@ -347,7 +354,12 @@ def gpu_run(args, world, rank, local):
     stream = torch.cuda.current_stream()
 
     def gather_into(w, full):
-        if nccl_group is None:
+        if rehearsal:
+            parts = [torch.empty(w.shape, dtype=w.dtype) for _ in range(world)]
+            dist.all_gather(parts, w.cpu())
+            if rank == 0:
+                full.copy_(torch.cat(parts))
+        elif nccl_group is None:
             V.bitmap_gather_device(w, full, root=0, stream=stream)
         else:
             parts = [torch.empty_like(w) for _ in range(world)]
@@ -475,7 +487,7 @@ def gpu_run(args, world, rank, local):
                 line["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)
     if world > 1:
-        if nccl_group is None:
+        if nccl_group is None and not rehearsal:
             V.comm_destroy()
         dist.destroy_process_group()
 
