@@ -148,6 +148,11 @@ def cpu_baseline(sig, msg, pk, threads_main, reps):
 def control_plane(world, rank):
     import torch.distributed as dist
     if world > 1:
+        # one node: gloo's and RCCL's bootstrap sockets on loopback, whoever
+        # launched the ranks (this launcher or the driver's torch.distributed.run)
+        # -- a hostname that does not resolve cannot stall the rendezvous
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo")
     return dist
 
