@@ -72,6 +72,11 @@ extern "C" {
  * accept bits; costs a hash pass and extra workspace (about 100 MB per
  * 2^20-signature chunk); does not pay when keys are all distinct. */
 #define STL_DEDUP_KEYS 0x8u
+/* A batch (or 2^20-signature chunk) with fewer signatures than half the
+ * device's resident lanes runs each signature on two lanes, which ends a
+ * launch that cannot fill the device sooner.  Same
+ * accept bits; this flag turns it off (A/B and tests). */
+#define STL_ONE_LANE 0x10u
 
 /* stl_config.flags.  With two or more devices the host batch calls gather the
  * accept bitmap on device 0 with RCCL over xGMI (ncclGather / grouped
@@ -105,8 +110,8 @@ const char *stl_strerror(int rc);
  * crypto_sign_verify_detached (0 = accept, -1 = reject), plus stellard's S<L:
  * i.e. exactly RippleAddress::verifySignature's bool as 0/-1.  Runs on the GPU
  * (batch of one); returns a value < -1 on a device error.
- * LATENCY: one signature is one GPU lane, so a call is latency-bound: 643 us
- * per call on MI355X against libsodium's 31 us, and concurrent calls
+ * LATENCY: a signature is one GPU lane pair, so a call is latency-bound: 561 us
+ * per call on MI355X against libsodium's 32 us, and concurrent calls
  * serialise on the device (tools/latency.py).
  * Callers that verify one signature at a time (stellard's JobQueue workers)
  * keep libsodium, or submit through stl_batcher_* when many requests are in

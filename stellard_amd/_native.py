@@ -31,6 +31,7 @@ STL_POLICY_MASK = 0x1
 STL_REQUIRE_S_LT_L = 0x2
 STL_FULL_LENGTH = 0x4
 STL_DEDUP_KEYS = 0x8
+STL_ONE_LANE = 0x10
 
 # per-transaction status of the serialized-transaction entry points
 STL_TX_OK = 0

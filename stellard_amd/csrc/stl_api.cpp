@@ -390,6 +390,17 @@ uint32_t grid_for(const Device& d, size_t n) {
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(tiles, d.grid));
 }
 
+// Per-lane workspace slots (workgroups) for launch_verify: room for two lanes
+// per signature when the batch is small enough to run that way.
+uint32_t verify_grid_for(const Device& d, size_t n) {
+  const size_t tiles = (n + stl::kBlock - 1) / stl::kBlock;
+  return (uint32_t)std::max<size_t>(1, std::min<size_t>(2 * tiles, d.grid));
+}
+
+// Largest chunk launch_verify runs on two lanes per signature: one pair wave
+// per SIMD at most (a quarter of the resident lanes).
+uint32_t pair_max(const Device& d) { return d.grid * stl::kBlock / 4; }
+
 // Contiguous 64-aligned shard of [0, n) for shard r of g (stl_shard_range).
 void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
   const size_t words = (n + 63) / 64;
@@ -547,8 +558,8 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
                                   static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream, b.kind));
     STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
                                static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, static_cast<uint4*>(d.ws.p),
-                               grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream,
-                               dev_counters(d), phase_clock(d)));
+                               verify_grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream,
+                               dev_counters(d), phase_clock(d), pair_max(d)));
   }
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
   if (dtxid) STL_TRY(hipMemcpyAsync(b.txid + 32 * lo, dtxid, n * 32, hipMemcpyDeviceToHost, d.stream));
@@ -627,7 +638,7 @@ int gather_to_host(const Batch& b, std::vector<Shard>& sh, size_t n, size_t per,
 }
 
 int check_flags(uint32_t flags) {
-  return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS)) ? STL_EINVAL : STL_OK;
+  return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS | STL_ONE_LANE)) ? STL_EINVAL : STL_OK;
 }
 
 int run_batch(const Batch& b, size_t n, uint64_t* gather_ns) {
@@ -949,7 +960,7 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
     STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                                static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
                                STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true,
-                               static_cast<const uint4*>(d.wide.p), s, dev_counters(d), phase_clock(d)));
+                               static_cast<const uint4*>(d.wide.p), s, dev_counters(d), phase_clock(d), pair_max(d)));
     STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
     STL_TRY(hipStreamSynchronize(s));
     return STL_OK;
@@ -982,8 +993,8 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   uint4* ws = nullptr;
   STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
-                             phase_clock(*d)));
+                             verify_grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
+                             phase_clock(*d), pair_max(*d)));
   return STL_OK;
 }
 
@@ -999,8 +1010,8 @@ int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const ui
   uint4* ws = nullptr;
   STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
   STL_TRY(stl::launch_verify(d_sig, d_k, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
-                             phase_clock(*d)));
+                             verify_grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
+                             phase_clock(*d), pair_max(*d)));
   return STL_OK;
 }
 

@@ -155,7 +155,7 @@ struct stl_batcher {
 extern "C" {
 
 stl_batcher* stl_batcher_create(uint32_t max_batch, uint32_t max_delay_us, uint32_t flags) {
-  if (max_batch == 0 || (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS))) return nullptr;
+  if (max_batch == 0 || (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS | STL_ONE_LANE))) return nullptr;
   stl_batcher* b = new (std::nothrow) stl_batcher();
   if (!b) return nullptr;
   b->max_batch = max_batch;

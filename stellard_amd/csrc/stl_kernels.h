@@ -37,16 +37,24 @@ inline size_t verify_ws_bytes(uint32_t grid, bool dedup = false) {
 }
 
 // Kernel mode word: bit 0 = policy (STL_POLICY_*), bit 8 = full-length path
-// for every lane (STL_FULL_LENGTH), bit 9 = per-batch key dedup (STL_DEDUP_KEYS).
+// for every lane (STL_FULL_LENGTH), bit 9 = per-batch key dedup (STL_DEDUP_KEYS),
+// bit 10 = never two lanes per signature (STL_ONE_LANE).
 constexpr uint32_t kModeFullLength = 0x100u;
 constexpr uint32_t kModeDedupKeys = 0x200u;
+constexpr uint32_t kModeOneLane = 0x400u;
 inline uint32_t kernel_mode(uint32_t flags) {
-  return (flags & 0x1u) | ((flags & 0x4u) ? kModeFullLength : 0u) | ((flags & 0x8u) ? kModeDedupKeys : 0u);
+  return (flags & 0x1u) | ((flags & 0x4u) ? kModeFullLength : 0u) | ((flags & 0x8u) ? kModeDedupKeys : 0u) |
+         ((flags & 0x10u) ? kModeOneLane : 0u);
 }
 
 const void* kernel_verify_msg32();
 // counters (nullable): device u64 [0] accept bits written, [1] lanes checked by
 // the full-length fallback path (stl_get_stats)
+// pair_max: chunks of at most this many signatures (and 2x as many workspace
+// lanes in `grid`) run two lanes per signature (verify_main_pair_kernel);
+// the caller passes a quarter of the device's resident lanes, i.e. at most one
+// pair wave per SIMD -- above that the duplicated doublings cost more than the
+// shorter chains save.
 // Optional phase clock (stl_set_phase_timing): launch_verify calls
 // mark(ctx, stream, i) before a chunk's first kernel (i = 0) and after each
 // phase -- 1 scalar, 2 point (+ the key-dedup kernels), 3 main, 4 fallback.
@@ -57,7 +65,7 @@ struct PhaseClock {
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k, const uint4* wide,
                          hipStream_t stream, unsigned long long* counters = nullptr,
-                         const PhaseClock* clock = nullptr);
+                         const PhaseClock* clock = nullptr, uint32_t pair_max = 0);
 hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t* m, const uint64_t* moff,
                            const uint64_t* mlen, uint32_t n, uint8_t* k_out, hipStream_t stream);
 // counter: one device word of scratch (reset by the launcher); grid: upper

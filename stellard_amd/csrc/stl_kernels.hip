@@ -559,6 +559,50 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
   }
 }
 
+// Phase 2 for small batches (2 x cnt lanes fit in one round of resident
+// lanes, no key dedup): lanes 2j and 2j+1 run signature j's two half chains
+// (verify_phase2_pair_chain) on one table each, swap their sums across the
+// pair, and both test that they cancel.  A wave decides 32 signatures: the
+// even bits of its ballot are one 32-bit half of a bitmap word (the other
+// half is the next wave's, in the same tile).
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_pair_kernel(
+    const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
+    uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr) {
+  TableView tab, unused;
+  lane_tables(ws, tab, unused);
+  __shared__ uint4 tails[9][kBlock];
+  tab.tail = &tails[0][threadIdx.x];
+  tab.tstride = kBlock;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const int par = (int)(lane & 1u);
+  WideGlobal wl{wide, {0, 0}};
+  const uint32_t words = (cnt + 63) >> 6;
+  for (uint32_t tile = blockIdx.x * kBlock; tile < 2 * cnt; tile += gridDim.x * kBlock) {
+    const uint32_t t = (tile + threadIdx.x) >> 1;  // signature of this lane pair
+    const bool live = t < cnt;
+    HalfState h;
+    ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
+    ge_p2 mine, other;
+    verify_phase2_pair_chain(mine, h, par, tab, wl);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      other.X.v[i] = (uint32_t)__shfl_xor((int)mine.X.v[i], 1);
+      other.Y.v[i] = (uint32_t)__shfl_xor((int)mine.Y.v[i], 1);
+      other.Z.v[i] = (uint32_t)__shfl_xor((int)mine.Z.v[i], 1);
+    }
+    const bool ok = live && half_state_accepts(h) && pair_sums_cancel(mine, other);
+    const uint64_t ball = __ballot(ok);
+    uint32_t half = 0;  // the even lanes' bits, compressed
+#pragma unroll
+    for (int b = 0; b < 32; ++b) half |= (uint32_t)((ball >> (2 * b)) & 1u) << b;
+    const uint32_t wsig = (tile + wave * 64) >> 1;  // first signature of this wave, a multiple of 32
+    if (lane == 0 && (wsig >> 6) < words) {
+      reinterpret_cast<uint32_t*>(bitmap)[(base + wsig) >> 5] = half;
+      if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popc(half));  // accepted (stl_get_stats)
+    }
+  }
+}
+
 // Full-length path for the lanes phase 1 flagged (rare: the lattice
 // reduction did not fit 2^131).  Waves with no flagged lane skip their tile;
 // flagged lanes OR their exact bit into the word phase 2 wrote.
@@ -1022,7 +1066,7 @@ hipError_t launch_wide_table(uint4* out, hipStream_t stream) {
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
                          const uint4* wide, hipStream_t stream, unsigned long long* counters,
-                         const PhaseClock* clock) {
+                         const PhaseClock* clock, uint32_t pair_max) {
   if (n == 0) return hipSuccess;
   auto mark = [&](int i) {
     if (clock) clock->mark(clock->ctx, stream, i);
@@ -1075,8 +1119,16 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
     mark(2);
-    hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
-                       counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr);
+    // Small chunks: two lanes per signature (verify_main_pair_kernel); the
+    // bits are the same.
+    const bool pair =
+        !dedup && (policy & kModeOneLane) == 0 && cnt <= pair_max && 2ull * cnt <= (uint64_t)grid * kBlock;
+    if (pair)
+      hipLaunchKernelGGL(verify_main_pair_kernel, dim3((2 * cnt + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, pre,
+                         base, cnt, bitmap, slots, wide, counters);
+    else
+      hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
+                         counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr);
     mark(3);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,

@@ -688,5 +688,84 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
   return (p.tops & kHalfOk) != 0 && (p.tops & kHalfFallback) == 0 && id;
 }
 
+// Small batches (fewer signatures than half the resident lanes): one
+// signature on two lanes.  Lane `par` = 0 runs [e_lo]B + [c]P1 (the low
+// wide table), lane 1 runs [e_hi]2^128 B + [d]P2 (the high one), on the same
+// doubling schedule as verify_phase2_half -- one table, one add per position
+// and one madd per fourth position instead of two each.  The pair then checks
+// that its two sums cancel (pair_sums_cancel).  Same accept bits; about 0.77x
+// of a lane's chain, so a launch whose lanes are not all busy ends sooner.
+template <typename Wide>
+STL_HD void verify_phase2_pair_chain(ge_p2& out, const HalfState& p, int par, const TableView& tab, Wide& wide) {
+  {
+    ge_p3 P;
+    affine_to_p3(P, par ? p.P2x : p.P1x, par ? p.P2y : p.P1y);
+    build_cached_table(tab, P);
+  }
+  const int npos = half_positions((int)(p.tops & 0xffu));
+  uint32_t dg[5], ed[4];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) dg[i] = par ? p.ddig[i] : p.cdig[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ed[i] = par ? p.edig[4 + i] : p.edig[i];
+  ge_p3 acc;
+  ge_p2 acc2;
+  ge_p1p1 t;
+  ge_p3_0(acc);
+  ge_p2_0(acc2);
+  uint32_t w = 0, we = 0;
+#pragma unroll 1
+  for (int i = kHalfDigits - 1; i >= 0; --i) {
+    if ((i & 7) == 7) {
+      w = dg[4];
+#pragma unroll
+      for (int m = 4; m > 0; --m) dg[m] = dg[m - 1];
+    }
+    if ((i & 7) == 4 && i < 32) {
+      we = ed[3];
+#pragma unroll
+      for (int m = 3; m > 0; --m) ed[m] = ed[m - 1];
+    }
+    const int d = (int32_t)w >> 28;
+    w <<= 4;
+    const bool bpos = (i & 3) == 0 && i < 32;  // wave-uniform
+    int de = 0;
+    if (bpos) de = (i & 4) ? (int32_t)we >> 16 : (int32_t)(we << 16) >> 16;
+    if (i >= npos) continue;  // wave-uniform
+    ge_cached c;
+    tab.load(d < 0 ? -d : d, c);  // issued ahead of the doublings, as in verify_phase2_half
+    if (bpos) wide.prefetch(par ? 0 : de, par ? de : 0);
+    if (i != npos - 1) dbl4(acc, acc2);
+    ge_cached_cneg(c, d < 0);
+    ge_add_cached(t, acc, c);
+    if (!bpos) {
+      ge_p1p1_to_p2(acc2, t);
+    } else {
+      ge_p1p1_to_p3(acc, t);
+      wide.madd(t, acc, par);
+      ge_p1p1_to_p2(acc2, t);
+    }
+  }
+  out = acc2;
+}
+
+// a + b == O  <=>  a == -b  <=>  Xa Zb == -Xb Za and Ya Zb == Yb Za (Z != 0).
+STL_HD bool pair_sums_cancel(const ge_p2& a, const ge_p2& b) {
+  fe l, r, s;
+  fe_mul(l, a.X, b.Z);
+  fe_mul(r, b.X, a.Z);
+  fe_add(s, l, r);
+  fe_carry(s);
+  const bool xs = fe_iszero(s);
+  fe_mul(l, a.Y, b.Z);
+  fe_mul(r, b.Y, a.Z);
+  fe_sub(s, l, r);
+  return xs && fe_iszero(s);
+}
+
+STL_HD bool half_state_accepts(const HalfState& p) {
+  return (p.tops & kHalfOk) != 0 && (p.tops & kHalfFallback) == 0;
+}
+
 
 }  // namespace stl

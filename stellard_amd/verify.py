@@ -25,6 +25,7 @@ POLICY_STELLARD_1_0_0 = N.STL_POLICY_STELLARD_1_0_0
 FULL_LENGTH = N.STL_FULL_LENGTH
 # OR into `policy` to decode each distinct public key of a batch once
 DEDUP_KEYS = N.STL_DEDUP_KEYS
+ONE_LANE = N.STL_ONE_LANE
 
 
 class BadInputs(RuntimeError):

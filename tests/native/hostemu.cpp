@@ -152,6 +152,47 @@ uint64_t hostemu_verify_batch_split(const uint8_t* sig, const uint8_t* msg, cons
   return g_bound_viol.load();
 }
 
+// The small-batch pair path of verify_main_kernel: each signature's two
+// chains (verify_phase2_pair_chain, parity 0 and 1, each on its own split
+// table with the kernel's LDS tail stride) and the pair's cancellation check.
+uint64_t hostemu_verify_batch_pair(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
+                                   uint8_t* bitmap, uint32_t policy) {
+  const int tstride = 256;
+  std::vector<uint4> heads(2 * 8 * 8), tails((size_t)9 * tstride + 1), id(9);
+  stl::ge_cached idc;
+  stl::ge_cached_0(idc);
+  stl::TableView::contiguous(id.data()).store(0, idc);
+  const stl::TableView t0 = stl::TableView::split(heads.data(), tails.data(), id.data(), tstride),
+                       t1 = stl::TableView::split(heads.data() + 64, tails.data() + 1, id.data(), tstride);
+  std::vector<uint4> full(81);
+  const stl::TableView tf = stl::TableView::contiguous(full.data());
+  const uint32_t* btab = &stl::kBaseNielsHost[0][0][0];
+  std::memset(bitmap, 0, (n + 7) / 8);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t R[8], S[8], A[8], M[8], h[16], k[8];
+    load8(R, sig + 64 * i);
+    load8(S, sig + 64 * i + 32);
+    load8(A, pk + 32 * i);
+    load8(M, msg + 32 * i);
+    stl::sha512_hram32(h, R, A, M);
+    stl::sc_reduce64(k, h);
+    stl::HalfState hs;
+    stl::verify_phase1_half(hs, R, S, A, k, policy);
+    bool ok;
+    if (hs.tops & stl::kHalfFallback) {
+      ok = stl::verify_full_with_k(R, S, A, k, policy, tf, btab);
+    } else {
+      stl::WideHost w0{wide_tables(), {0, 0}}, w1{wide_tables(), {0, 0}};
+      stl::ge_p2 a, b;
+      stl::verify_phase2_pair_chain(a, hs, 0, t0, w0);
+      stl::verify_phase2_pair_chain(b, hs, 1, t1, w1);
+      ok = stl::half_state_accepts(hs) && stl::pair_sums_cancel(a, b) && stl::pair_sums_cancel(b, a);
+    }
+    if (ok) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  return g_bound_viol.load();
+}
+
 // Words of the identity entry's head as the split tables expect it (the
 // device constant kIdentityHead must equal these 32 words).
 void hostemu_identity_head(uint32_t out[32]) {

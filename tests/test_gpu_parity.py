@@ -166,6 +166,35 @@ def test_ragged_sizes(stl, golden, n):
     assert np.array_equal(got, golden["expected_sodium_1_0_18"][idx].astype(bool))
 
 
+def test_pair_lanes_same_bits(stl, oracle, torch_cuda):
+    """Batches up to a quarter of the resident lanes run each signature on two lanes
+    (verify_main_pair_kernel); STL_ONE_LANE forces one lane.  Both give the
+    oracle's bits on mutated rows at ragged sizes either side of the switch,
+    on the host and device APIs; the accept counter counts the pair path's
+    bits once.  Pre-filled output words show that every word of the batch is
+    written (bits past n included)."""
+    torch = torch_cuda
+    n = 70000
+    sig, msg, pk = _gpu_signed(stl, torch, n, 4711)
+    rng = np.random.default_rng(17)
+    s, m, p = _mutate(sig.cpu().numpy(), msg.cpu().numpy(), pk.cpu().numpy(), rng)
+    exp = oracle.verify_batch(s, m, p, threads=16)
+    ds, dm, dp = (torch.from_numpy(a).cuda() for a in (s, m, p))
+    for k in (1, 31, 33, 95, 4097, 32767, 32768, 32769, 65537, 70000):
+        two = stl.verify_batch(s[:k], m[:k], p[:k])
+        one = stl.verify_batch(s[:k], m[:k], p[:k], policy=stl.ONE_LANE)
+        assert np.array_equal(two, exp[:k]), (k, np.nonzero(two != exp[:k])[0][:10])
+        assert np.array_equal(one, exp[:k]), k
+        w = torch.full(((k + 63) // 64,), -1, dtype=torch.int64, device="cuda")
+        stl.reset_stats()
+        stl.verify_batch_device(ds[:k], dm[:k], dp[:k], out_words=w)
+        torch.cuda.synchronize()
+        assert stl.get_stats()["accepted"] == int(exp[:k].sum()), k
+        bits = np.unpackbits(w.cpu().numpy().astype("<i8").view(np.uint8), bitorder="little")
+        assert np.array_equal(bits[:k].astype(bool), exp[:k]), k
+        assert not bits[k:].any(), k
+
+
 def test_empty_batch(stl):
     z = np.zeros((0, 64), np.uint8)
     assert stl.verify_batch(z, np.zeros((0, 32), np.uint8), np.zeros((0, 32), np.uint8)).size == 0

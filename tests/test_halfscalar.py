@@ -186,6 +186,23 @@ def test_split_table_layout_vs_golden(emu, golden, policy, key, tstride):
     assert np.array_equal(got, golden[key].astype(bool))
 
 
+@pytest.mark.parametrize("policy,key", [(0, "expected_sodium_1_0_18"), (1, "expected_stellard_1_0_0_unpinned")])
+def test_pair_chains_vs_golden(emu, golden, policy, key):
+    """The small-batch pair path (verify_phase2_pair_chain on two lanes,
+    [e_lo]B + [c]P1 and [e_hi]2^128 B + [d]P2, then pair_sums_cancel) gives
+    the golden bits."""
+    sig, msg, pk = golden["sig"], golden["msg"], golden["pk"]
+    n = sig.shape[0]
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    B = lambda a: np.ascontiguousarray(a).ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    viol = emu.hostemu_verify_batch_pair(B(sig), B(msg), B(pk), n, B(bm), policy)
+    assert viol == 0
+    got = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    exp = golden[key].astype(bool)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, [(int(i), str(golden["class_names"][golden["cls"][i]])) for i in bad[:10]]
+
+
 def test_identity_head_constant(emu):
     """kIdentityHead (stl_kernels.hip) holds the identity entry's head as the
     split tables store it: YpX = YmX = Z = 1, T2d = 0, 9 limbs each."""

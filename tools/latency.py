@@ -102,18 +102,37 @@ def main():
 
             bat_call(0)
             rep[f"stl_batcher_max_delay_{delay}us"] = [threaded(bat_call, 6, 300), threaded(bat_call, 64, 200)]
-    sizes = {}
-    for m in (1, 64, 1024, 16384, 65536):
-        V.verify_batch(sig[:m], msg[:m], pk[:m])
-        ts = []
-        for _ in range(5):
-            t0 = time.perf_counter()
-            ok = V.verify_batch(sig[:m], msg[:m], pk[:m])
-            ts.append(time.perf_counter() - t0)
-        assert ok.all()
-        t = float(np.median(ts))
-        sizes[str(m)] = {"ms": t * 1e3, "verifies_per_s": m / t}
-    rep["stl_ed25519_verify_batch_by_size"] = sizes
+    # batches below half the resident lanes run two lanes per signature;
+    # STL_ONE_LANE is the one-lane A/B of the same call
+    for label, pol in (("", 0), ("_one_lane", V.ONE_LANE)):
+        sizes = {}
+        for m in (1, 64, 1024, 16384, 65536):
+            V.verify_batch(sig[:m], msg[:m], pk[:m], policy=pol)
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                ok = V.verify_batch(sig[:m], msg[:m], pk[:m], policy=pol)
+                ts.append(time.perf_counter() - t0)
+            assert ok.all()
+            t = float(np.median(ts))
+            sizes[str(m)] = {"ms": t * 1e3, "verifies_per_s": m / t}
+        rep["stl_ed25519_verify_batch_by_size" + label] = sizes
+        dev = {}  # device-resident inputs: kernels only (HIP events on the call's stream)
+        for m in (1, 1024, 16384, 32768, 65536):
+            w = torch.empty((m + 63) // 64, dtype=torch.int64, device="cuda")
+            V.verify_batch_device(sig_d[:m], msgs[:m], pk_d[:m], out_words=w, policy=pol)
+            ts = []
+            for _ in range(9):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                V.verify_batch_device(sig_d[:m], msgs[:m], pk_d[:m], out_words=w, policy=pol,
+                                      stream=torch.cuda.current_stream())
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            assert V.words_to_bool(w, m).all()
+            dev[str(m)] = {"ms": float(np.median(ts))}
+        rep["stl_ed25519_verify_batch_device_by_size" + label] = dev
     doc = json.dumps(rep, indent=1)
     print(doc)
     if args.out:
