@@ -110,7 +110,7 @@ const char *stl_strerror(int rc);
  * crypto_sign_verify_detached (0 = accept, -1 = reject), plus stellard's S<L:
  * i.e. exactly RippleAddress::verifySignature's bool as 0/-1.  Runs on the GPU
  * (batch of one); returns a value < -1 on a device error.
- * LATENCY: a signature is one GPU lane pair, so a call is latency-bound: 561 us
+ * LATENCY: a signature is one GPU lane pair, so a call is latency-bound: 489 us
  * per call on MI355X against libsodium's 32 us, and concurrent calls
  * serialise on the device (tools/latency.py).
  * Callers that verify one signature at a time (stellard's JobQueue workers)

@@ -216,6 +216,56 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_point_k
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
 
+// verify_point_kernel for small chunks (the pair chunks of
+// verify_main_pair_kernel): lanes 2j and 2j+1 decode signature j's A and R,
+// one square-root chain each, swap the results and finish together; lane 0
+// writes the state, a wave's even ballot bits are a 32-bit half of a
+// fallback word.  At most one wave per SIMD runs it (pair_max), so it takes
+// the registers of 2 waves/SIMD and does not spill.
+__global__ __launch_bounds__(kBlock, 2) void verify_point_pair_kernel(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk, uint32_t base, uint32_t cnt, uint32_t policy,
+    uint4* __restrict__ pre, uint64_t* __restrict__ fb_words) {
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t t = g >> 1;
+  const int par = (int)(g & 1u);
+  const bool live = t < cnt;
+  const uint32_t tt = live ? t : cnt - 1;
+  const size_t j = (size_t)base + tt;
+  uint32_t R[8], S[8], A[8];
+  ld8(R, sig + 64 * j);
+  ld8(S, sig + 64 * j + 32);
+  ld8(A, pk + 32 * j);
+  uint4* q = pre + (size_t)tt * 14;
+  HalfState h;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&h);
+  const uint4 q2 = q[kHalfTopsWord / 4];
+  w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+  fe mx, my, ox, oy;
+  const bool mok = phase1_decode_lane(mx, my, R, A, par);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    ox.v[i] = (uint32_t)__shfl_xor((int)mx.v[i], 1);
+    oy.v[i] = (uint32_t)__shfl_xor((int)my.v[i], 1);
+  }
+  const bool ook = __shfl_xor((int)mok, 1) != 0;
+  if (par == 0)
+    phase1_points_finish_pair(h, R, S, A, policy & 1u, mx, my, mok, ox, oy, ook);
+  else
+    phase1_points_finish_pair(h, R, S, A, policy & 1u, ox, oy, ook, mx, my, mok);
+  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  if (live && par == 0) {
+    st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
+#pragma unroll
+    for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+  }
+  const uint64_t ball = __ballot(live && (h.tops & kHalfFallback) != 0);
+  uint32_t half = 0;
+#pragma unroll
+  for (int b = 0; b < 32; ++b) half |= (uint32_t)((ball >> (2 * b)) & 1u) << b;
+  const uint32_t wsig = (g & ~63u) >> 1;  // first signature of this wave, a multiple of 32
+  if ((threadIdx.x & 63u) == 0 && (wsig >> 6) < ((cnt + 63) >> 6)) reinterpret_cast<uint32_t*>(fb_words)[wsig >> 5] = half;
+}
+
 // ---- per-batch key dedup (STL_DEDUP_KEYS) ----
 // stellard's signers repeat (configs 1 and 5: 1,000 accounts for 100k
 // transactions), so the batch decodes each distinct key once:
@@ -1092,6 +1142,11 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     const dim3 g1((cnt + kBlock - 1) / kBlock);
     const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
     const dim3 g2(tiles < grid ? tiles : grid);
+    // Small chunks: two lanes per signature in the point and main kernels
+    // (verify_point_pair_kernel, verify_main_pair_kernel); the bits are the same.
+    const bool pair =
+        !dedup && (policy & kModeOneLane) == 0 && cnt <= pair_max && 2ull * cnt <= (uint64_t)grid * kBlock;
+    const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
     mark(0);
     if (pre_k)
       hipLaunchKernelGGL(verify_scalar_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
@@ -1115,17 +1170,15 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
                            dim3(kBlock), 0, stream, counter, cnt, keytab, widetabs);
       hipLaunchKernelGGL(verify_point_kernel_keyed, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb,
                          rep, uid_of, keytab, counter);
+    } else if (pair) {
+      hipLaunchKernelGGL(verify_point_pair_kernel, gp, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     } else {
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
     mark(2);
-    // Small chunks: two lanes per signature (verify_main_pair_kernel); the
-    // bits are the same.
-    const bool pair =
-        !dedup && (policy & kModeOneLane) == 0 && cnt <= pair_max && 2ull * cnt <= (uint64_t)grid * kBlock;
     if (pair)
-      hipLaunchKernelGGL(verify_main_pair_kernel, dim3((2 * cnt + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, pre,
-                         base, cnt, bitmap, slots, wide, counters);
+      hipLaunchKernelGGL(verify_main_pair_kernel, gp, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
+                         counters);
     else
       hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
                          counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr);

@@ -433,6 +433,28 @@ STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32
   finish_phase1_points(o, negA.X, negA.Y, negQ.X, negQ.Y, ok);
 }
 
+// Small batches: verify_phase1_points on a lane pair, one decoding per lane
+// (`par` 0 decodes A, 1 decodes R, into -A / -Q); the pair swaps the results
+// and both lanes finish with phase1_points_finish_pair.
+STL_HD bool phase1_decode_lane(fe& nx, fe& ny, const uint32_t R[8], const uint32_t A[8], int par) {
+  uint32_t P[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) P[i] = par ? R[i] : A[i];
+  ge_p3 n;
+  const bool ok = ge_frombytes_negate_vartime(n, P);
+  nx = n.X;
+  ny = n.Y;
+  return ok;
+}
+
+STL_HD void phase1_points_finish_pair(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
+                                      uint32_t policy, const fe& nAx, const fe& nAy, bool okA, const fe& nQx,
+                                      const fe& nQy, bool okR) {
+  bool ok = verify_prechecks(R, S, A, policy);
+  ok = ok && sc_lt_L(S) && r_is_canonical(R) && okA && okR;
+  finish_phase1_points(o, nAx, nAy, nQx, nQy, ok);
+}
+
 // Phase 1, point half, with -A decoded once per distinct key of the batch
 // (STL_DEDUP_KEYS: many transactions share a signer): decodes only R.  The
 // key's decoding is a function of its 32 bytes alone, so the result is the

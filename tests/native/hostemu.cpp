@@ -152,7 +152,8 @@ uint64_t hostemu_verify_batch_split(const uint8_t* sig, const uint8_t* msg, cons
   return g_bound_viol.load();
 }
 
-// The small-batch pair path of verify_main_kernel: each signature's two
+// The small-batch pair path (verify_point_pair_kernel +
+// verify_main_pair_kernel): each signature's two decodings, its two
 // chains (verify_phase2_pair_chain, parity 0 and 1, each on its own split
 // table with the kernel's LDS tail stride) and the pair's cancellation check.
 uint64_t hostemu_verify_batch_pair(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
@@ -177,7 +178,10 @@ uint64_t hostemu_verify_batch_pair(const uint8_t* sig, const uint8_t* msg, const
     stl::sha512_hram32(h, R, A, M);
     stl::sc_reduce64(k, h);
     stl::HalfState hs;
-    stl::verify_phase1_half(hs, R, S, A, k, policy);
+    stl::verify_phase1_scalars(hs, S, k);
+    stl::fe ax, ay, qx, qy;  // the pair's two decodings (verify_point_pair_kernel)
+    const bool okA = stl::phase1_decode_lane(ax, ay, R, A, 0), okR = stl::phase1_decode_lane(qx, qy, R, A, 1);
+    stl::phase1_points_finish_pair(hs, R, S, A, policy, ax, ay, okA, qx, qy, okR);
     bool ok;
     if (hs.tops & stl::kHalfFallback) {
       ok = stl::verify_full_with_k(R, S, A, k, policy, tf, btab);
