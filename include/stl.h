@@ -70,7 +70,9 @@ extern "C" {
 /* Decode each distinct public key of a batch once (stellard's signers repeat:
  * the configs-1/5 shape is 1,000 accounts for 100k transactions).  Same
  * accept bits; costs a hash pass and extra workspace (about 100 MB per
- * 2^20-signature chunk); does not pay when keys are all distinct. */
+ * 2^20-signature chunk); does not pay when keys are all distinct.  Chunks
+ * small enough for lane pairs (STL_ONE_LANE below) run on pairs instead:
+ * latency-bound there, the pairs are faster. */
 #define STL_DEDUP_KEYS 0x8u
 /* A batch (or 2^20-signature chunk) with fewer signatures than half the
  * device's resident lanes runs each signature on two lanes, which ends a

@@ -509,10 +509,12 @@ def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
     # 20,000 rows over the 525 golden keys (>= 32 rows per key): the wide
     # per-key tables (c's digits in radix-256 pairs); 8,000 rows: the 9-entry
     # per-key tables
+    # (STL_ONE_LANE: batches this small otherwise run on lane pairs, no dedup)
     for rows in (20000, 8000):
         idx = np.random.default_rng(3).integers(0, sig.shape[0], rows)
-        got = stl.verify_batch(sig[idx], msg[idx], pk[idx], policy=policy | stl.DEDUP_KEYS)
-        assert np.array_equal(got, golden[key][idx].astype(bool)), rows
+        for extra in (stl.ONE_LANE, 0):
+            got = stl.verify_batch(sig[idx], msg[idx], pk[idx], policy=policy | stl.DEDUP_KEYS | extra)
+            assert np.array_equal(got, golden[key][idx].astype(bool)), (rows, extra)
     # 1,000 signers, (1 << 20) + 4099 rows: two chunks, keys shared across both
     n = (1 << 20) + 4099
     rng = np.random.default_rng(5)

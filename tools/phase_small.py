@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--signers", type=int, default=0, help="distinct keys (0 = every row its own)")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -26,13 +27,19 @@ def main():
     V.init(device_count=1)
     n = 1 << 16
     rng = np.random.default_rng(0x1A7)
-    seeds = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    seeds_np = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    if args.signers:
+        seeds_np = seeds_np[rng.integers(0, args.signers, n)]
+    seeds = torch.from_numpy(seeds_np).cuda()
     msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
     pk, sig = V.sign_batch_device(seeds, msgs)
     torch.cuda.synchronize()
     rep = {}
     V.set_phase_timing(True)
-    for label, pol in (("pair", 0), ("one_lane", V.ONE_LANE)):
+    modes = [("pair", 0), ("one_lane", V.ONE_LANE)]
+    if args.signers:
+        modes += [("dedup", V.DEDUP_KEYS), ("dedup_one_lane", V.DEDUP_KEYS | V.ONE_LANE)]
+    for label, pol in modes:
         for m in (1, 1024, 16384, 32768):
             w = torch.empty((m + 63) // 64, dtype=torch.int64, device="cuda")
             V.verify_batch_device(sig[:m], msgs[:m], pk[:m], out_words=w, policy=pol)
@@ -44,6 +51,7 @@ def main():
             st = V.get_stats()
             assert V.words_to_bool(w, m).all()
             rep[f"{label}_{m}"] = {k: v / 1e3 / args.reps for k, v in st["phase_ns"].items()}  # us per call
+            rep[f"{label}_{m}"]["total"] = sum(rep[f"{label}_{m}"].values())
             print(label, m, {k: round(v, 1) for k, v in rep[f"{label}_{m}"].items()}, flush=True)
     V.set_phase_timing(False)
     if args.out:
