@@ -1148,6 +1148,10 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     // latency-bound, and measured 0.46-0.52 ms on pairs against 0.68-0.75 ms
     // deduplicated (1,000 signers).
     const bool pair = (policy & kModeOneLane) == 0 && cnt <= pair_max && 2ull * cnt <= (uint64_t)grid * kBlock;
+    // The point kernel's pairs split its two square roots without duplicating
+    // work, so they pay up to twice that size (two pair waves per SIMD; no
+    // workspace), ahead of the one-lane main kernel.
+    const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
     const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
     mark(0);
     if (pre_k)
@@ -1155,7 +1159,7 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     else
       hipLaunchKernelGGL(verify_scalar_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     mark(1);
-    if (pair) {
+    if (pair_point) {
       hipLaunchKernelGGL(verify_point_pair_kernel, gp, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     } else if (dedup) {
       uint32_t nslots = 64;

@@ -169,7 +169,8 @@ def test_ragged_sizes(stl, golden, n):
 def test_pair_lanes_same_bits(stl, oracle, torch_cuda):
     """Batches up to a quarter of the resident lanes run each signature on two lanes
     (verify_main_pair_kernel); STL_ONE_LANE forces one lane.  Both give the
-    oracle's bits on mutated rows at ragged sizes either side of the switch,
+    oracle's bits on mutated rows at ragged sizes either side of the switches
+    (the point kernel pairs up to twice the main kernel's limit),
     on the host and device APIs; the accept counter counts the pair path's
     bits once.  Pre-filled output words show that every word of the batch is
     written (bits past n included)."""
@@ -180,7 +181,7 @@ def test_pair_lanes_same_bits(stl, oracle, torch_cuda):
     s, m, p = _mutate(sig.cpu().numpy(), msg.cpu().numpy(), pk.cpu().numpy(), rng)
     exp = oracle.verify_batch(s, m, p, threads=16)
     ds, dm, dp = (torch.from_numpy(a).cuda() for a in (s, m, p))
-    for k in (1, 31, 33, 95, 4097, 32767, 32768, 32769, 65537, 70000):
+    for k in (1, 31, 33, 95, 4097, 32767, 32768, 32769, 49153, 65536, 65537, 70000):
         two = stl.verify_batch(s[:k], m[:k], p[:k])
         one = stl.verify_batch(s[:k], m[:k], p[:k], policy=stl.ONE_LANE)
         assert np.array_equal(two, exp[:k]), (k, np.nonzero(two != exp[:k])[0][:10])

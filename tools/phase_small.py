@@ -40,7 +40,7 @@ def main():
     if args.signers:
         modes += [("dedup", V.DEDUP_KEYS), ("dedup_one_lane", V.DEDUP_KEYS | V.ONE_LANE)]
     for label, pol in modes:
-        for m in (1, 1024, 16384, 32768):
+        for m in (1, 1024, 16384, 32768, 49152, 65536):
             w = torch.empty((m + 63) // 64, dtype=torch.int64, device="cuda")
             V.verify_batch_device(sig[:m], msgs[:m], pk[:m], out_words=w, policy=pol)
             torch.cuda.synchronize()
