@@ -1151,7 +1151,11 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     // The point kernel's pairs split its two square roots without duplicating
     // work, so they pay up to twice that size (two pair waves per SIMD; no
     // workspace), ahead of the one-lane main kernel.
+#ifdef STL_POINT_PAIR_ALL
+    const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup);
+#else
     const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
+#endif
     const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
     mark(0);
     if (pre_k)
