@@ -89,3 +89,19 @@ def test_batcher_rejects_bad_arguments():
     assert not lib.stl_batcher_create(0, 100, 0)
     assert not lib.stl_batcher_create(16, 100, 0x80)
     assert lib.stl_batcher_submit(None, bytes(64), bytes(32), bytes(32), None, None) == N.STL_EINVAL
+
+
+def test_flag_validation():
+    """Every STL_* verify flag of stl.h is accepted (STL_ONE_LANE included);
+    an unknown bit is STL_EINVAL before any device work, on every box."""
+    import ctypes
+    from stellard_amd import _native as N
+    lib = N.load()
+    sig, msg, pk, bm = bytes(64), bytes(32), bytes(32), ctypes.create_string_buffer(1)
+    for flags in (0, N.STL_POLICY_STELLARD_1_0_0, N.STL_FULL_LENGTH, N.STL_DEDUP_KEYS, N.STL_ONE_LANE,
+                  N.STL_DEDUP_KEYS | N.STL_ONE_LANE):
+        assert lib.stl_ed25519_verify_batch(sig, msg, pk, 1, bm, flags) != N.STL_EINVAL, flags
+    assert lib.stl_ed25519_verify_batch(sig, msg, pk, 1, bm, 0x20) == N.STL_EINVAL
+    b = lib.stl_batcher_create(16, 100, N.STL_ONE_LANE)
+    assert b
+    lib.stl_batcher_destroy(b)
