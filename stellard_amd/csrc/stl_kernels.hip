@@ -661,6 +661,14 @@ __global__ __launch_bounds__(kBlock, 2) void verify_fallback_kernel(
     const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
     uint32_t base, uint32_t cnt, uint32_t policy, const uint64_t* __restrict__ fb_words,
     uint64_t* __restrict__ bitmap, uint4* __restrict__ ws, unsigned long long* __restrict__ ctr) {
+  // A workgroup none of whose tiles has a flagged lane (almost all of them)
+  // ends before staging the base table.
+  int any = 0;
+  for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
+    const uint32_t wbase = tile + (threadIdx.x >> 6) * 64;
+    if ((threadIdx.x & 63u) == 0 && wbase < cnt && fb_words[wbase >> 6] != 0) any = 1;
+  }
+  if (!__syncthreads_or(any)) return;  // workgroup-uniform
   __shared__ uint32_t sB[kBaseTableWords];
   stage_base_table(sB, 1);
   TableView tab, unused;
