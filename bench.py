@@ -100,9 +100,16 @@ def launch(args):
 
 
 # ------------------------------------------------------------ cpu baseline
-def cpu_baseline(sig, msg, pk, threads_main, reps):
+def affinity_cpus():
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
+def cpu_baseline(sig, msg, pk, threads_share, reps):
     """Host-core baseline on bounded samples of the same workload, median of
-    `reps` runs per thread count (T = box CPU share, 6, 1)."""
+    `reps` runs per thread count: T = the CPUs this process may run on
+    (len(sched_getaffinity), SURVEY 8d's "nproc of the GPU box"; the headline
+    `value`/`cores`), the box's CPU share (16), 6 (stellard's JobQueue
+    default) and 1."""
     from tests import oracle_bind
     lib = oracle_bind.load_sodium_ref()
     if lib is not None:
@@ -119,17 +126,20 @@ def cpu_baseline(sig, msg, pk, threads_main, reps):
 
         def run(s, m, p, t):
             return o.verify_batch(s, m, p, threads=t)
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    tmain = max(1, threads_main)
+    avail = affinity_cpus()
+    tmain = max(1, avail)
     # bounded samples: about 1 s of CPU work per run at each thread count
-    plan = [(tmain, 1 << 19), (JOBQUEUE_THREADS, 1 << 18), (1, 1 << 15)]
+    # (the whole batch at T = affinity: 16-256 threads on the box)
+    plan = [(tmain, 1 << 20), (max(1, threads_share), 1 << 19), (JOBQUEUE_THREADS, 1 << 18), (1, 1 << 15)]
     rates = {}
     for t, cap in plan:
+        if str(t) in rates:
+            continue
         n = min(cap, sig.shape[0])
         s, m, p = (np.ascontiguousarray(a[:n]) for a in (sig, msg, pk))
         run(s[:256], m[:256], p[:256], t)  # warm
         times, acc = [], None
-        for _ in range(reps):
+        for _ in range(reps):  # noqa: B007
             t0 = time.perf_counter()
             bits = run(s, m, p, t)
             times.append(time.perf_counter() - t0)
@@ -139,9 +149,151 @@ def cpu_baseline(sig, msg, pk, threads_main, reps):
     main_rate = rates[str(tmain)]["verifies_per_s"]
     return {"value": main_rate, "unit": "verifies/s", "cores": tmain, "kind": kind,
             "sample": f"first {rates[str(tmain)]['sample']} signatures of the bench batch at T={tmain} "
-                      f"(the box's CPU share; also T=6 = stellard JobQueue default and T=1 below), median of "
+                      f"(= len(sched_getaffinity), the CPUs this process may use; also T={threads_share} = the "
+                      f"box's CPU share, T=6 = stellard JobQueue default and T=1 under by_threads), median of "
                       f"{reps}; {what}",
             "by_threads": rates, "host_nproc": os.cpu_count(), "host_affinity_cpus": avail}
+
+
+def end_to_end(V, torch, sig, msgs, pk, reps=5):
+    """SURVEY 8d timing (ii): the host batch API on the bench batch --
+    stl_ed25519_verify_batch from host buffers: H2D copies, the verify
+    kernels, the bitmap D2H (libstl pipelines the copies with the kernels) --
+    from pinned (page-locked) and from ordinary pageable memory, median of
+    `reps` calls each.  Never `value`."""
+    import ctypes
+    from stellard_amd import _native as N
+    n = sig.shape[0]
+    out = {"n": n, "reps": reps}
+    B = lambda a: ctypes.c_void_p(a.data_ptr()) if hasattr(a, "data_ptr") else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    ref = None
+    for kind in ("pinned", "pageable"):
+        if kind == "pinned":
+            h = [torch.empty(t.shape, dtype=torch.uint8, pin_memory=True) for t in (sig, msgs, pk)]
+            for d, t in zip(h, (sig, msgs, pk)):
+                d.copy_(t)
+            bm = torch.zeros((n + 7) // 8, dtype=torch.uint8, pin_memory=True)
+        else:
+            h = [np.ascontiguousarray(t.cpu().numpy()) for t in (sig, msgs, pk)]
+            bm = np.zeros((n + 7) // 8, np.uint8)
+        lib = N.load()
+        call = lambda: N.check(lib.stl_ed25519_verify_batch(B(h[0]), B(h[1]), B(h[2]), n, B(bm), 0),  # noqa: E731
+                               "stl_ed25519_verify_batch")
+        call()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        bits = np.unpackbits(np.asarray(bm.numpy() if hasattr(bm, "numpy") else bm), bitorder="little")[:n]
+        ref = bits if ref is None else ref
+        med = float(np.median(ts))
+        out[kind] = {"verifies_per_s": n / med, "ms": med * 1e3, "all_accepted": bool(bits.all()),
+                     "bits_equal_pinned": bool((bits == ref).all())}
+    out["timing"] = ("host steady clock around each stl_ed25519_verify_batch call (H2D of 128 B/signature + "
+                     "kernels + D2H of the bitmap, PCIe-inclusive)")
+    return out
+
+
+def config1_leg(V, torch, dev, stream, threads_share, n=100_000, nacc=1000, seed=0x5EED0001):
+    """BASELINE configs[0] / SURVEY 8d config 1: 100,000 synthetic Payment
+    transactions of 1,000 accounts as whole serialized blobs (Appendix C,
+    175-220 B), checkSign from the bytes: libstl's device-resident
+    stl_tx_blob_prepare_device + verify, its host API stl_tx_blob_verify_batch
+    (PCIe-inclusive), and the reference's own path on the host CPUs --
+    parse, re-serialise, OpenSSL SHA-512, libsodium verify && S<L
+    (SerializedTransaction.cpp:220-230, Serializer.cpp:354-360,
+    RippleAddress.cpp:190-200; oracle/_ref/libsodium_ref.so's
+    ref_tx_blob_verify_batch) at T = affinity / box share / 6 / 1."""
+    import ctypes
+    from tests import oracle_bind
+    from tools.payments import blobs_from_preimages, pack, payment_preimages
+    from stellard_amd import _native as N
+    rng = np.random.default_rng(seed)
+    acc_seeds = rng.integers(0, 256, (nacc, 32), dtype=np.uint8)
+    apk, _ = V.sign_batch_device(torch.from_numpy(acc_seeds).to(dev), torch.zeros((nacc, 32), dtype=torch.uint8,
+                                                                                    device=dev))
+    apk = apk.cpu().numpy()
+    pre = payment_preimages(apk, n, rng)
+    pbuf, poff, plen = pack(pre)
+    d_msg = V.tx_hash_batch_device(torch.from_numpy(pbuf).to(dev), torch.from_numpy(poff.view(np.int64)).to(dev),
+                                   torch.from_numpy(plen.view(np.int32)).to(dev), stream=stream)
+    seeds = torch.from_numpy(acc_seeds[np.arange(n) % nacc]).to(dev)
+    tpk, tsig = V.sign_batch_device(seeds, d_msg)
+    torch.cuda.synchronize()
+    blobs = blobs_from_preimages(pre, tsig.cpu().numpy(), tpk.cpu().numpy())
+    buf, offs, lens = pack(blobs)
+    buf = np.concatenate([buf, np.zeros(4, np.uint8)])
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    words = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+
+    def device_call():
+        o = V.tx_blob_prepare_device(d_buf, d_off, d_len, tx_ids=False, stream=stream)
+        V.verify_batch_device(o["sig"], o["msg"], o["pk"], out_words=words, stream=stream)
+        return o
+
+    o = device_call()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(7):
+        t0 = time.perf_counter()
+        device_call()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    dev_s = float(np.median(ts))
+    dev_bits = V.words_to_bool(words, n)
+    status_ok = int((o["status"].cpu().numpy() == V.TX_OK).sum())
+    B = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    st = np.zeros(n, np.uint8)
+    lib = N.load()
+    host = lambda: N.check(lib.stl_tx_blob_verify_batch(B(buf), B(offs), B(lens), n, B(bm), B(st), None, 0),  # noqa: E731
+                           "stl_tx_blob_verify_batch")
+    host()
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        host()
+        ts.append(time.perf_counter() - t0)
+    host_s = float(np.median(ts))
+    host_bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    out = {"n": n, "accounts": nacc, "blob_bytes": {"min": int(lens.min()), "median": int(np.median(lens)),
+                                                   "max": int(lens.max())},
+           "gpu_device_resident_tx_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
+           "gpu_host_api_tx_per_s": n / host_s, "gpu_host_api_ms": host_s * 1e3, "status_ok": status_ok,
+           "gpu_timing": "host clock around prepare + verify on the stream + sync (device-resident), or around "
+                         "one stl_tx_blob_verify_batch call (host API); median"}
+    lib_ref = oracle_bind.load_sodium_ref()
+    if lib_ref is None:
+        out["cpu_reference"] = None
+        return out
+    cpu = {}
+    ref_bits = None
+    for t, cap in ((affinity_cpus(), n), (threads_share, n), (JOBQUEUE_THREADS, 50_000), (1, 10_000)):
+        if str(t) in cpu:
+            continue
+        m = min(cap, n)
+        run = lambda: oracle_bind.sodium_tx_blob_verify_batch(lib_ref, blobs[:m], threads=t)  # noqa: E731
+        run()
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            bits = run()
+            ts.append(time.perf_counter() - t0)
+        if m == n and ref_bits is None:
+            ref_bits = bits
+        cpu[str(t)] = {"tx_per_s": m / float(np.median(ts)), "sample": m, "median_s": float(np.median(ts))}
+    out["cpu_reference"] = {"by_threads": cpu, "kind": "reference",
+                            "what": "ref_tx_blob_verify_batch: parse + re-serialise (oracle/stl_oracle_tx.c) + "
+                                    "OpenSSL SHA512 + libsodium 1.0.18 crypto_sign_verify_detached && S<L, "
+                                    "std::thread-style static partition, median of 3"}
+    if ref_bits is not None:
+        out["bitmap_parity"] = {"rows": n, "accepted": int(ref_bits.sum()),
+                                "mismatches_device": int((dev_bits != ref_bits).sum()),
+                                "mismatches_host_api": int((host_bits != ref_bits).sum())}
+    return out
 
 
 # ------------------------------------------------------------------ ranks
@@ -189,7 +341,9 @@ def dry_run(args, world, rank):
             "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u32", "data": "synthetic", "dry_run": True,
             "config": {"workload": "dry run", "signatures_per_gpu": n, "parallelism": f"dp{world}",
-                       "rank0_shard": [lo, hi], "gathered_all_ones": ok},
+                       "rank0_shard": [lo, hi], "gathered_all_ones": ok,
+                       "rccl_nranks": world, "rccl_nranks_source": "stub (dry run: no RCCL communicator; the GPU "
+                                                                   "run reads libstl's stl_comm_info)"},
             "roofline": None, "cpu_baseline": None}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -317,6 +471,7 @@ def gpu_run(args, world, rank, local):
     assert (lo, hi) == (rank * n, (rank + 1) * n) or n % 64, "per-rank shards are whole ballot words"
     gather_via = None
     nccl_group = None
+    rccl_nranks = None
     if rehearsal:
         gather_via = "gloo through host memory (rehearsal of the multi-rank flow, not the RCCL product path)"
     elif world > 1:
@@ -346,6 +501,12 @@ def gpu_run(args, world, rank, local):
             gather_via = "torch.distributed nccl all_gather (libstl RCCL init failed: %s)" % next(e for e in errs if e)
         else:
             gather_via = "libstl stl_bitmap_gather_device (ncclGather to rank 0)"
+            # what RCCL itself says the communicator is (ncclCommCount /
+            # ncclCommUserRank): every rank must see all N ranks before timing
+            rccl_nranks, rccl_rank = V.comm_info()
+            if rccl_nranks != world or rccl_rank != rank:
+                raise SystemExit(f"rank {rank}: RCCL communicator reports rank {rccl_rank} of {rccl_nranks}, "
+                                 f"WORLD_SIZE={world}")
 
     # ---- synthetic data (outside the timed region) ----
     rng = np.random.default_rng(0x5EED0002 + rank)
@@ -389,7 +550,7 @@ def gpu_run(args, world, rank, local):
 
     # ---- timed region: exactly K steps between barrier+sync on both sides ----
     torch.cuda.synchronize()
-    V.set_phase_timing(True)  # HIP events between the verify phases of every launch (stl_stats.phase_ns)
+    V.set_phase_timing(False)
     V.reset_stats()
     if world > 1:
         dist.barrier()
@@ -414,6 +575,16 @@ def gpu_run(args, world, rank, local):
         assert V.words_to_bool(full_words, n * world).all(), "gathered bitmap has rejects"
 
     st = V.get_stats()  # device counters over the K timed launches (after the sync above)
+    # ---- per-kernel timing pass (after the timed region): K more launches with
+    # libstl's phase clock -- HIP events recorded on the launch stream between
+    # the kernels of each launch, which runs its kernels one after another (no
+    # concurrent chunks), so each duration is that kernel's alone ----
+    V.set_phase_timing(True)
+    V.reset_stats()
+    for _ in range(args.steps):
+        V.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
+    torch.cuda.synchronize()
+    pst = V.get_stats()
     V.set_phase_timing(False)
     extra = None
     if not args.no_extra:
@@ -421,8 +592,8 @@ def gpu_run(args, world, rank, local):
             extra = extra_configs(world, rank, dist, V, torch, dev, stream, sig, msgs, pk, gather_into)
         except Exception as e:  # noqa: BLE001 - the extra legs must not cost the bench line
             extra = {"error": f"rank {rank}: {e!r}"}
-    chunks = max(1, st["phase_chunks"])
-    phase_ms = {k: v / chunks / 1e6 for k, v in st["phase_ns"].items()}  # average per launch (one chunk each)
+    chunks = max(1, pst["phase_chunks"])
+    phase_ms = {k: v / chunks / 1e6 for k, v in pst["phase_ns"].items()}  # average per launch (one chunk each)
     if rank == 0:
         total = n * world * args.steps
         value = total / dt
@@ -463,19 +634,21 @@ def gpu_run(args, world, rank, local):
                        "signatures_per_gpu": n,
                        "parallelism": f"dp{world} (index shards, RCCL bitmap gather to rank 0)"
                                       if world > 1 else "dp1",
-                       "gather": gather_via},
+                       "gather": gather_via, "rccl_nranks": rccl_nranks,
+                       "execution": V.execution_settings()},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
                          "kernel": "verify_main_kernel (dominant: %.0f %% of the launch)"
                                    % (100.0 * main_ms / max(1e-9, sum(phase_ms.values()))),
                          "kernel_ms": main_ms, "work_per_verify": W_VERIFY, "units_per_launch": n,
-                         "timing": "libstl phase events (stl_set_phase_timing) on the launch stream over the "
-                                   "K timed launches; work = W_VERIFY x n per launch attributed to the main kernel",
+                         "timing": "libstl phase events (stl_set_phase_timing) on the launch stream over K "
+                                   "launches right after the timed region (kernels one after another); work = "
+                                   "W_VERIFY x n per launch attributed to the main kernel",
                          "phase_ms": phase_ms,
                          "launch_ms": kern_ms, "achieved_launch": achieved_launch,
                          "frac_launch": achieved_launch * 1e12 / PEAK_INT_OPS,
-                         "launch": "verify_scalar + verify_point + verify_main + verify_fallback, one stream, HIP "
-                                   "events around each stl_ed25519_verify_batch_device call",
+                         "launch": "every kernel of one stl_ed25519_verify_batch_device call (phase 1, main, "
+                                   "fallback), HIP events around each call of the timed region",
                          "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9),
                          "valu_busy_pmc": valu_busy},
             "cpu_baseline": None,
@@ -484,6 +657,17 @@ def gpu_run(args, world, rank, local):
                       "verifies": n * args.steps},
             "extra_configs": extra,
         }
+        if world == 1:
+            try:
+                line["end_to_end"] = end_to_end(V, torch, sig, msgs, pk)
+            except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench line
+                line["end_to_end"] = {"error": repr(e)}
+        if world == 1 and not args.no_extra:
+            try:
+                c1 = config1_leg(V, torch, dev, stream, args.cpu_threads)
+            except Exception as e:  # noqa: BLE001
+                c1 = {"error": repr(e)}
+            line["extra_configs"] = dict(line["extra_configs"] or {}, config1_payment_checksign_100k=c1)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(sig.cpu().numpy(), msgs.cpu().numpy(), pk.cpu().numpy(),

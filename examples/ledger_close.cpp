@@ -80,8 +80,10 @@ int main(int argc, char** argv) {
   const size_t n = txs.size();
 
   // 1. process init
+  // stellard passes libsodium's crypto_sign_verify_detached as fallback_verify;
+  // this example does not link libsodium, so single calls report device errors
   stl_config cfg = {sizeof(stl_config), /*device_count*/ 0, /*first_device*/ 0, /*flags*/ 0,
-                    /*shards_per_device*/ 1, 0};
+                    /*shards_per_device*/ 1, 0, /*fallback_verify*/ nullptr};
   const int init_rc = stl_init(&cfg);
   std::printf("stl_init %d (%s) devices %d %s\n", init_rc, stl_strerror(init_rc), stl_device_count(), stl_version());
 

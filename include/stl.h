@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define STL_ABI_VERSION 2
+#define STL_ABI_VERSION 3
 
 /* ---- return codes ---- */
 #define STL_OK 0
@@ -69,32 +69,56 @@ extern "C" {
 #define STL_FULL_LENGTH 0x4u
 /* Decode each distinct public key of a batch once (stellard's signers repeat:
  * the configs-1/5 shape is 1,000 accounts for 100k transactions).  Same
- * accept bits; costs a hash pass and extra workspace (about 100 MB per
- * 2^20-signature chunk); does not pay when keys are all distinct.  Chunks
- * small enough for lane pairs (STL_ONE_LANE below) run on pairs instead:
- * latency-bound there, the pairs are faster. */
+ * accept bits; costs a hash pass and extra device workspace: about 270 MB
+ * (stl_kernels.h kDedupBytes: hash slots, key arrays, decoded keys, shared and
+ * wide key tables), allocated once per device for the host batch API and once
+ * per (device, stream) -- per library stream too -- for the device-resident
+ * API; does not pay when keys are all distinct.  Chunks small enough for lane
+ * pairs (STL_ONE_LANE below) run on pairs instead: latency-bound there, the
+ * pairs are faster. */
 #define STL_DEDUP_KEYS 0x8u
-/* A batch (or 2^20-signature chunk) with fewer signatures than half the
- * device's resident lanes runs each signature on two lanes, which ends a
- * launch that cannot fill the device sooner.  Same
- * accept bits; this flag turns it off (A/B and tests). */
+/* Small chunks run each signature on two lanes, which ends a launch that
+ * cannot fill the device sooner: the main kernel up to
+ * a quarter of the device's resident lanes (one pair wave per SIMD; 32,768
+ * signatures on 256 CUs), the point decoding up to half of them.  Same accept
+ * bits; this flag turns it off (A/B and tests). */
 #define STL_ONE_LANE 0x10u
+/* TEST-ONLY: the raw crypto_sign_verify_detached predicate of the selected
+ * policy, without stellard's S < L -- what RippleAddress_test expects of the
+ * bare libsodium call (RippleAddress.cpp:838-845: under the 1.0.0 policy a
+ * signature with S + L verifies).  stellard's accept is always the composite;
+ * never set this outside tests. */
+#define STL_DEBUG_RAW_PREDICATE 0x80000000u
 
-/* stl_config.flags.  With two or more devices the host batch calls gather the
- * accept bitmap on device 0 with RCCL over xGMI (ncclGather / grouped
- * send-recv into one buffer) and copy it to the host once; stl_init returns
- * STL_ERCCL if that communicator cannot be built. */
-#define STL_CFG_RCCL_GATHER 0x1u /* use the RCCL gather even with one device */
+/* stl_config.flags.  By default every device of a host batch call copies its
+ * slice of the accept bitmap to the host.  With STL_CFG_RCCL_GATHER the slices
+ * are gathered on device 0 with RCCL over xGMI (ncclGather / grouped
+ * send-recv into one buffer, any device count) and copied to the host once;
+ * stl_init returns STL_ERCCL if that communicator cannot be built.  (Opt-in
+ * until a multi-GPU run has compared the gathered bitmaps: the one-process-
+ * per-GPU gather, stl_bitmap_gather_device, is the measured path.) */
+#define STL_CFG_RCCL_GATHER 0x1u /* gather the bitmap over RCCL (in-process communicator) */
 #define STL_CFG_NO_RCCL 0x2u     /* never use RCCL: every device copies its slice to the host */
 
+/* The caller's own single-signature check, libsodium's signature:
+ * stellard passes crypto_sign_verify_detached (libstl never links it). */
+typedef int (*stl_verify_fn)(const unsigned char *sig, const unsigned char *m, unsigned long long mlen,
+                             const unsigned char *pk);
+
 typedef struct stl_config {
-  uint32_t struct_size;       /* sizeof(stl_config); the 16-byte ABI-1 struct is accepted too */
+  uint32_t struct_size;       /* sizeof(stl_config); the 16-byte ABI-1 and 24-byte ABI-2 structs
+                                 are accepted too */
   int32_t device_count;       /* devices to use; <= 0 = all visible */
   int32_t first_device;       /* first HIP ordinal to use */
   uint32_t flags;             /* STL_CFG_* */
   int32_t shards_per_device;  /* ABI 2: host batch shards per device, each on its own host
                                  thread (<= 0 = 1; more than 1 forces the per-device copy) */
   uint32_t reserved;          /* 0 */
+  stl_verify_fn fallback_verify; /* ABI 3, may be NULL: with it, stl_ed25519_verify_detached
+                                    answers a device failure (ENODEV, ENOMEM, EHIP, ERCCL)
+                                    with fallback_verify(...) == 0 && S < L, so it returns
+                                    only 0 or -1 -- libsodium's convention.  Registered even
+                                    when stl_init itself then fails for want of a device. */
 } stl_config;
 
 /* Replaces/augments sodium_init() (src/ripple_app/ripple_app.cpp:129-132).
@@ -108,10 +132,16 @@ int stl_device_count(void);
 const char *stl_version(void);
 const char *stl_strerror(int rc);
 
-/* Same signature and return convention as libsodium's
- * crypto_sign_verify_detached (0 = accept, -1 = reject), plus stellard's S<L:
- * i.e. exactly RippleAddress::verifySignature's bool as 0/-1.  Runs on the GPU
- * (batch of one); returns a value < -1 on a device error.
+/* Same signature as libsodium's crypto_sign_verify_detached (0 = accept,
+ * -1 = reject), plus stellard's S<L: i.e. exactly
+ * RippleAddress::verifySignature's bool as 0/-1.  Runs on the GPU (batch of
+ * one).  A device failure returns a value < -1 -- unless stl_config's
+ * fallback_verify was registered, in which case the call answers with it and
+ * only ever returns 0 or -1.  Only with a fallback registered is this a
+ * literal drop-in for `crypto_sign_verify_detached(...) == 0` at
+ * RippleAddress.cpp:196-197: without one a device error must be told apart
+ * from a reject by the caller (rc < -1).  STL_EINVAL (a NULL pointer) is
+ * returned either way.
  * LATENCY: a signature is one GPU lane pair, so a call is latency-bound: 489 us
  * per call on MI355X against libsodium's 32 us, and concurrent calls
  * serialise on the device (tools/latency.py).
@@ -213,6 +243,12 @@ int stl_signed_blob_prepare_device(uint32_t kind, const uint8_t *d_blobs, const 
 int stl_comm_unique_id(uint8_t id[128]);
 int stl_comm_init_rank(int nranks, int rank, const uint8_t id[128]);
 void stl_comm_destroy(void);
+/* What RCCL itself reports for the communicator libstl gathers over
+ * (ncclCommCount / ncclCommUserRank): the one-process-per-GPU communicator of
+ * stl_comm_init_rank if there is one, else the in-process communicator of
+ * stl_init (the rank of the calling thread's current device).  STL_ERCCL when
+ * there is neither. */
+int stl_comm_info(int *nranks, int *rank);
 /* root >= 0: ncclGather of every rank's d_words (words_per_rank u64 words)
  * into d_all_words on rank root (nranks*words_per_rank words, rank order;
  * other ranks may pass NULL); root < 0: ncclAllGather (every rank receives).
@@ -276,9 +312,11 @@ typedef struct stl_stats {
   /* Phase timing (stl_set_phase_timing(1) or STL_PHASE_TIMING=1; zero when
    * off): summed kernel time of the verify phases, measured with HIP events
    * recorded on the launch stream between the phases of every chunk (at most
-   * 2^20 signatures) -- [0] scalar (SHA-512 + lattice), [1] point
-   * decompression (with the key-dedup kernels), [2] main (Straus loop),
-   * [3] fallback -- and the number of chunks timed. */
+   * 2^20 signatures; a timed launch runs its chunks one after another) --
+   * [0] phase 1 (the whole of it when it runs as one kernel, the default;
+   * SHA-512 + lattice when split, STL_TUNE_FUSED_PREP 0), [1] the point
+   * decompression kernel when split and the key-dedup kernels, [2] main
+   * (Straus loop), [3] fallback -- and the number of chunks timed. */
   uint64_t phase_ns[4];
   uint64_t phase_chunks;
 } stl_stats;
@@ -300,12 +338,37 @@ void stl_debug_fault_after(long long calls);
  * next to ordinary lanes in one wave. */
 int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const uint8_t *d_pk, size_t n,
                               uint64_t *d_bitmap_words, uint32_t flags, void *stream);
+/* Execution tuning, process-wide, for A/B experiments and tests: every setting
+ * gives the same accept bits.  Returns the previous value, or STL_EINVAL for
+ * an unknown key or a value out of range; value -1 only reads the setting.
+ * Takes effect for launches made after the call. */
+#define STL_TUNE_FUSED_PREP 0 /* 1 (default): phase 1 (SHA-512, lattice, decodings) as one kernel; 0: two */
+#define STL_TUNE_MAIN_QUEUE 1 /* 1 (default): the main kernel's waves pull 64-signature units from a
+                                 counter; 0: static grid stride */
+#define STL_TUNE_STREAMS 2    /* 1..4: a device-resident verify call runs its chunks on this many
+                                 concurrent streams (the caller's plus the library's own, forked
+                                 and joined by events; not under stl_set_phase_timing) */
+#define STL_TUNE_CHUNK_LOG2 3 /* 16..20: log2 of the signatures per chunk when STL_TUNE_STREAMS > 1 */
+#define STL_TUNE_BYTE_SHARDS 4 /* 1: host preimage / blob batches take the byte-balanced shard path even
+                                  as one shard (test hook: runs the grouped-gather placement and
+                                  rank 0's device copy on one GPU under STL_CFG_RCCL_GATHER) */
+int stl_debug_tuning(int key, int value);
 
 /* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;
  * EdKeyPair::setSeed, EdKeyPair.cpp:25-33): RFC 8032 keypair from a 32-byte
  * seed and a detached signature over a 32-byte message. */
 int stl_ed25519_sign_batch_device(const uint8_t *d_seed, const uint8_t *d_msg, size_t n, uint8_t *d_pk,
                                   uint8_t *d_sig, void *stream);
+/* Test data only: the same rows, then row i with d_cls[i] in 1..11 mutated
+ * into SURVEY.md Appendix-B class B<cls> with the 32-bit parameter
+ * d_param[i] (the construction of tests/datasets.py, stated in
+ * stl_kernels.hip adversarial_row: bit flips, S+L, S >= 2^253, small-order
+ * keys and R, mixed-order keys re-signed over A+T, non-canonical and off-curve
+ * keys, non-canonical R); d_msg_out receives every row's message (d_cls[i] = 0
+ * leaves the row honest). */
+int stl_debug_sign_adversarial_device(const uint8_t *d_seed, const uint8_t *d_msg, const uint8_t *d_cls,
+                                      const uint32_t *d_param, size_t n, uint8_t *d_pk, uint8_t *d_sig,
+                                      uint8_t *d_msg_out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -168,3 +168,13 @@ void ref_sign_batch(const uint8_t *seed, const uint8_t *msg, size_t n, uint8_t *
   }
   for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
 }
+
+/* Group operations for the adversarial rows of the committed datasets
+ * (tests/datasets.py: B6 R = [S]B, B8 A' = A + T). */
+int ref_scalarmult_base_noclamp(unsigned char *q, const unsigned char *n) {
+  return crypto_scalarmult_ed25519_base_noclamp(q, n);
+}
+
+int ref_point_add(unsigned char *r, const unsigned char *p, const unsigned char *q) {
+  return crypto_core_ed25519_add(r, p, q);
+}

@@ -33,6 +33,13 @@ STL_FULL_LENGTH = 0x4
 STL_DEDUP_KEYS = 0x8
 STL_ONE_LANE = 0x10
 
+# stl_debug_tuning keys
+STL_TUNE_FUSED_PREP = 0
+STL_TUNE_MAIN_QUEUE = 1
+STL_TUNE_STREAMS = 2
+STL_TUNE_CHUNK_LOG2 = 3
+STL_TUNE_BYTE_SHARDS = 4
+
 # per-transaction status of the serialized-transaction entry points
 STL_TX_OK = 0
 STL_TX_DEFERRED = 1
@@ -72,6 +79,7 @@ SYMBOLS = [
     ("stl_comm_unique_id", ctypes.c_int, [_U8P]),
     ("stl_comm_init_rank", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _U8P]),
     ("stl_comm_destroy", None, []),
+    ("stl_comm_info", ctypes.c_int, [_P, _P]),
     ("stl_bitmap_gather_device", ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_int, _P]),
     ("stl_shard_range", None, [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _P, _P]),
     ("stl_shard_range_bytes", None, [_P, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _P, _P]),
@@ -80,6 +88,9 @@ SYMBOLS = [
     ("stl_reset_stats", None, []),
     ("stl_set_phase_timing", ctypes.c_int, [ctypes.c_int]),
     ("stl_debug_verify_k_device", ctypes.c_int, [_U8P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
+    ("stl_debug_tuning", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("stl_debug_sign_adversarial_device", ctypes.c_int,
+     [_U8P, _U8P, _U8P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, _P]),
 ]
 
 VERDICT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)

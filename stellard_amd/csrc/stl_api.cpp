@@ -26,6 +26,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -87,6 +88,8 @@ struct Rccl {
   decltype(&ncclRecv) Recv = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclCommCount) CommCount = nullptr;
+  decltype(&ncclCommUserRank) CommUserRank = nullptr;
 
   template <typename F>
   static bool sym(void* h, const char* name, F& f) {
@@ -102,7 +105,8 @@ struct Rccl {
       ok = sym(h, "ncclGetUniqueId", GetUniqueId) && sym(h, "ncclCommInitRank", CommInitRank) &&
            sym(h, "ncclCommInitAll", CommInitAll) && sym(h, "ncclCommDestroy", CommDestroy) &&
            sym(h, "ncclGather", Gather) && sym(h, "ncclAllGather", AllGather) && sym(h, "ncclSend", Send) &&
-           sym(h, "ncclRecv", Recv) && sym(h, "ncclGroupStart", GroupStart) && sym(h, "ncclGroupEnd", GroupEnd);
+           sym(h, "ncclRecv", Recv) && sym(h, "ncclGroupStart", GroupStart) && sym(h, "ncclGroupEnd", GroupEnd) &&
+           sym(h, "ncclCommCount", CommCount) && sym(h, "ncclCommUserRank", CommUserRank);
     });
     return ok;
   }
@@ -158,10 +162,17 @@ struct PhaseTimer {
     std::lock_guard<std::mutex> lk(mu);
     pool.push_back(e);
   }
-  // completed chunks -> sums (the caller has synchronised the device)
+  // completed chunks -> sums.  A chunk another thread enqueued after the
+  // caller's synchronisation is left in `done` until its last event has
+  // completed (hipEventQuery), so it is neither dropped nor recycled early.
   void collect() {
     std::lock_guard<std::mutex> lk(mu);
+    std::vector<std::array<hipEvent_t, 5>> pending;
     for (auto& c : done) {
+      if (hipEventQuery(c[4]) == hipErrorNotReady) {
+        pending.push_back(c);
+        continue;
+      }
       uint64_t t[4];
       bool ok = true;
       for (int i = 0; i < 4 && ok; ++i) {
@@ -175,7 +186,7 @@ struct PhaseTimer {
       }
       for (hipEvent_t e : c) pool.push_back(e);
     }
-    done.clear();
+    done.swap(pending);
   }
   void reset() {
     collect();
@@ -230,6 +241,43 @@ void phase_mark(void* ctx, hipStream_t s, int i) {
   }
 }
 
+// Execution tuning (stl_debug_tuning): how a verify launch is cut into kernels
+// and streams.  Every setting gives the same accept bits (tests run them all).
+std::atomic<int> g_tune_fused{1};     // phase 1 as one kernel
+std::atomic<int> g_tune_queue{1};     // main kernel pulls units from a counter
+std::atomic<int> g_tune_streams{1};   // concurrent streams per device-resident call
+std::atomic<int> g_tune_sub_log2{18}; // signatures per stream chunk
+std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
+
+// Verify workspaces of one caller stream: ws[0] for the caller's stream, and
+// with several streams per call (g_tune_streams) ws[j] for the library's own
+// stream aux[j], forked from and joined to the caller's by events.
+struct StreamCtx {
+  DevBuf ws[stl::kMaxVerifyStreams];
+  hipStream_t aux[stl::kMaxVerifyStreams] = {};
+  hipEvent_t fork = nullptr;
+  hipEvent_t join[stl::kMaxVerifyStreams] = {};
+  // Wait for everything issued on the library's streams (error paths).
+  void drain_aux() {
+    for (hipStream_t s : aux)
+      if (s) (void)hipStreamSynchronize(s);
+  }
+  void release() {
+    drain_aux();
+    for (auto& b : ws) b.release();
+    for (hipStream_t& s : aux) {
+      if (s) (void)hipStreamDestroy(s);
+      s = nullptr;
+    }
+    for (hipEvent_t& e : join) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+    if (fork) (void)hipEventDestroy(fork);
+    fork = nullptr;
+  }
+};
+
 struct Device {
   int ordinal = 0;
   int cus = 0;
@@ -238,10 +286,11 @@ struct Device {
   hipStream_t copy = nullptr;    // its host-to-device copies (overlap the previous chunk's kernels)
   ncclComm_t comm = nullptr;     // in-process communicator (rank = device index)
   std::mutex mu;
-  DevBuf ws, sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide, gather;
+  StreamCtx host;  // verify workspaces of the host batch API (on `stream`)
+  DevBuf sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide, gather;
   DevBuf counters;  // device u64 counters of stl_get_stats: [0] accepted, [1] full-length lanes
-  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ws;   // device-resident API
-  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;  // tx-hash work counter
+  std::map<hipStream_t, std::unique_ptr<StreamCtx>> stream_ws;  // device-resident API
+  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;    // tx-hash work counter
   std::mutex ws_mu;
   PhaseTimer timer;
   stl::PhaseClock clock{phase_mark, &timer};
@@ -255,6 +304,8 @@ std::vector<std::unique_ptr<Device>> g_devs;
 bool g_init = false;
 int g_shards_per_device = 1;
 bool g_comm_gather = false;  // host batches gather their bitmap over RCCL
+// the caller's own check for stl_ed25519_verify_detached's device failures
+std::atomic<stl_verify_fn> g_fallback_verify{nullptr};
 
 // one process per GPU (stl_comm_*)
 std::mutex g_pcomm_mu;
@@ -342,9 +393,10 @@ void release_device(Device& d) {
   if (d.copy) (void)hipStreamSynchronize(d.copy);
   if (d.comm && g_rccl.ok) (void)g_rccl.CommDestroy(d.comm);
   d.comm = nullptr;
-  for (DevBuf* b : {&d.ws, &d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.txid, &d.status,
+  for (DevBuf* b : {&d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.txid, &d.status,
                     &d.wide, &d.gather, &d.counters})
     b->release();
+  d.host.release();
   for (auto& kv : d.stream_ws) kv.second->release();
   for (auto& kv : d.stream_ctr) kv.second->release();
   d.timer.release();
@@ -361,13 +413,75 @@ int ensure_init() {
   return stl_init(nullptr);
 }
 
-// Workspace for (device, stream) pairs used by the device-resident API.
-int stream_workspace(Device& d, hipStream_t s, uint4** ws, bool dedup = false) {
+// Verify workspaces for (device, stream) pairs used by the device-resident API.
+StreamCtx& stream_ctx(Device& d, hipStream_t s) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
   auto& slot = d.stream_ws[s];
-  if (!slot) slot.reset(new DevBuf());
-  STL_RC(slot->ensure(stl::verify_ws_bytes(d.grid, dedup)));
-  *ws = static_cast<uint4*>(slot->p);
+  if (!slot) slot.reset(new StreamCtx());
+  return *slot;
+}
+
+// Per-lane workspace slots (workgroups) for launch_verify: room for two lanes
+// per signature when the batch is small enough to run that way.
+uint32_t verify_grid_for(const Device& d, size_t n) {
+  const size_t tiles = (n + stl::kBlock - 1) / stl::kBlock;
+  return (uint32_t)std::max<size_t>(1, std::min<size_t>(2 * tiles, d.grid));
+}
+
+// Largest chunk launch_verify runs on two lanes per signature: one pair wave
+// per SIMD at most (a quarter of the resident lanes).
+uint32_t pair_max(const Device& d) { return d.grid * stl::kBlock / 4; }
+
+unsigned long long* dev_counters(Device& d);
+const stl::PhaseClock* phase_clock(Device& d);
+
+// Execution plan of one launch_verify of n signatures on stream s: the
+// workspaces of context c (allocated on first use) and, with more than one
+// stream per call, the library's own streams and events (created on first
+// use).  `streams` > 1 only for the device-resident API: the host batch API
+// already overlaps its copies with the previous chunk's kernels.
+int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode, int streams, stl::VerifyExec& x) {
+  const bool dedup = (mode & stl::kModeDedupKeys) != 0;
+  x.grid = verify_grid_for(d, n);
+  x.pair_max = pair_max(d);
+  x.wide = static_cast<const uint4*>(d.wide.p);
+  x.counters = dev_counters(d);
+  x.clock = phase_clock(d);
+  x.fused_prep = g_tune_fused.load() != 0;
+  x.main_queue = g_tune_queue.load() != 0;
+  x.sub = 1u << g_tune_sub_log2.load();
+  uint32_t S = (uint32_t)std::max(1, std::min<int>(streams, (int)stl::kMaxVerifyStreams));
+  if (x.clock || n <= x.sub || x.sub <= x.pair_max) S = 1;
+  S = (uint32_t)std::min<size_t>(S, (n + x.sub - 1) / x.sub);
+  x.nstreams = S;
+  for (uint32_t j = 0; j < S; ++j) {
+    STL_RC(c.ws[j].ensure(stl::verify_ws_bytes(d.grid, dedup)));
+    x.ws[j] = static_cast<uint4*>(c.ws[j].p);
+    if (j == 0) {
+      x.streams[0] = s;
+      continue;
+    }
+    if (!c.aux[j]) STL_TRY(hipStreamCreateWithFlags(&c.aux[j], hipStreamNonBlocking));
+    if (!c.join[j]) STL_TRY(hipEventCreateWithFlags(&c.join[j], hipEventDisableTiming));
+    x.streams[j] = c.aux[j];
+    x.join[j] = c.join[j];
+  }
+  if (S > 1 && !c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+  x.fork = c.fork;
+  return STL_OK;
+}
+
+// launch_verify with the plan of verify_exec; on an error the library's own
+// streams are drained before returning (nothing may still run on the
+// caller's buffers outside the caller's stream).
+int run_verify(Device& d, StreamCtx& c, hipStream_t s, const uint8_t* sig, const uint8_t* msg_or_k,
+               const uint8_t* pk, size_t n, uint64_t* words, uint32_t mode, bool pre_k, int streams) {
+  stl::VerifyExec x;
+  STL_RC(verify_exec(d, c, s, n, mode, streams, x));
+  if (fault_now() || stl::launch_verify(sig, msg_or_k, pk, (uint32_t)n, words, mode, pre_k, x) != hipSuccess) {
+    c.drain_aux();
+    return STL_EHIP;
+  }
   return STL_OK;
 }
 
@@ -389,17 +503,6 @@ uint32_t grid_for(const Device& d, size_t n) {
   const size_t tiles = (n + stl::kBlock - 1) / stl::kBlock;
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(tiles, d.grid));
 }
-
-// Per-lane workspace slots (workgroups) for launch_verify: room for two lanes
-// per signature when the batch is small enough to run that way.
-uint32_t verify_grid_for(const Device& d, size_t n) {
-  const size_t tiles = (n + stl::kBlock - 1) / stl::kBlock;
-  return (uint32_t)std::max<size_t>(1, std::min<size_t>(2 * tiles, d.grid));
-}
-
-// Largest chunk launch_verify runs on two lanes per signature: one pair wave
-// per SIMD at most (a quarter of the resident lanes).
-uint32_t pair_max(const Device& d) { return d.grid * stl::kBlock / 4; }
 
 // Contiguous 64-aligned shard of [0, n) for shard r of g (stl_shard_range).
 void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
@@ -509,7 +612,6 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
   STL_TRY(hipSetDevice(d.ordinal));
   STL_RC(d.bitmap.ensure(std::max<size_t>(words_alloc, 1) * 8));
   if (n == 0) return STL_OK;
-  STL_RC(d.ws.ensure(stl::verify_ws_bytes(d.grid, (b.policy & stl::kModeDedupKeys) != 0)));
   STL_RC(d.sig.ensure(n * 64));
   STL_RC(d.msg.ensure(n * 32));
   STL_RC(d.pk.ensure(n * 32));
@@ -556,10 +658,8 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
       STL_TRY(stl::launch_tx_blob(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, dsig + 64 * c0,
                                   dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0,
                                   static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream, b.kind));
-    STL_TRY(stl::launch_verify(dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, (uint32_t)cn,
-                               static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, static_cast<uint4*>(d.ws.p),
-                               verify_grid_for(d, cn), false, static_cast<const uint4*>(d.wide.p), d.stream,
-                               dev_counters(d), phase_clock(d), pair_max(d)));
+    STL_RC(run_verify(d, d.host, d.stream, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
+                      static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, false, 1));
   }
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
   if (dtxid) STL_TRY(hipMemcpyAsync(b.txid + 32 * lo, dtxid, n * 32, hipMemcpyDeviceToHost, d.stream));
@@ -610,8 +710,11 @@ int gather_to_host(const Batch& b, std::vector<Shard>& sh, size_t n, size_t per,
   // (an injected fault stops here, before the group: a group that some ranks
   // join and others do not would never complete)
   STL_RCCL_TRY(g_rccl.GroupStart());
+  // every communicator's ops are posted even after a failed enqueue (the first
+  // error is kept): a group that some ranks join and others do not could hang
+  // in GroupEnd instead of returning
   int rc = STL_OK;
-  for (int r = 0; r < g && rc == STL_OK; ++r) {
+  for (int r = 0; r < g; ++r) {
     Device& d = *sh[r].d;
     const uint64_t* sbuf = static_cast<const uint64_t*>(d.bitmap.p);
     if (equal) {
@@ -619,9 +722,9 @@ int gather_to_host(const Batch& b, std::vector<Shard>& sh, size_t n, size_t per,
     } else {
       const size_t w = (sh[r].hi - sh[r].lo + 63) / 64;
       if (w == 0 || r == 0) continue;  // rank 0's own slice: a device copy below
-      if (g_rccl.Send(sbuf, w, ncclUint64, 0, d.comm, d.stream) != ncclSuccess ||
-          g_rccl.Recv(rbuf + sh[r].lo / 64, w, ncclUint64, r, root.comm, root.stream) != ncclSuccess)
-        rc = STL_ERCCL;
+      const bool sent = g_rccl.Send(sbuf, w, ncclUint64, 0, d.comm, d.stream) == ncclSuccess;
+      const bool recv = g_rccl.Recv(rbuf + sh[r].lo / 64, w, ncclUint64, r, root.comm, root.stream) == ncclSuccess;
+      if (!sent || !recv) rc = STL_ERCCL;
     }
   }
   if (g_rccl.GroupEnd() != ncclSuccess && rc == STL_OK) rc = STL_ERCCL;
@@ -638,7 +741,10 @@ int gather_to_host(const Batch& b, std::vector<Shard>& sh, size_t n, size_t per,
 }
 
 int check_flags(uint32_t flags) {
-  return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS | STL_ONE_LANE)) ? STL_EINVAL : STL_OK;
+  return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS | STL_ONE_LANE |
+                    STL_DEBUG_RAW_PREDICATE))
+             ? STL_EINVAL
+             : STL_OK;
 }
 
 int run_batch(const Batch& b, size_t n, uint64_t* gather_ns) {
@@ -652,7 +758,7 @@ int run_batch(const Batch& b, size_t n, uint64_t* gather_ns) {
   int gg = g * g_shards_per_device;
   while ((n + gg - 1) / gg > kMaxShard) gg += g;
   std::vector<size_t> bound;
-  const bool by_bytes = b.mode != Mode::kSig && gg > 1;
+  const bool by_bytes = b.mode != Mode::kSig && (gg > 1 || g_tune_byte_shards.load() != 0);
   if (by_bytes) shard_bytes_bounds(b.len, n, gg, bound);
   std::vector<Shard> sh(gg);
   for (int r = 0; r < gg; ++r) {
@@ -719,8 +825,9 @@ int stl_init(const stl_config* cfg) {
   int first = 0, want = -1, spd = 1;
   uint32_t cflags = 0;
   if (cfg) {  // argument checks first: they need no device
-    const uint32_t abi1 = 4 * sizeof(uint32_t);
-    if (cfg->struct_size != sizeof(stl_config) && cfg->struct_size != abi1) return STL_EINVAL;
+    const uint32_t abi1 = 4 * sizeof(uint32_t), abi2 = offsetof(stl_config, fallback_verify);
+    const uint32_t sz = cfg->struct_size;
+    if (sz != sizeof(stl_config) && sz != abi1 && sz != abi2) return STL_EINVAL;
     first = cfg->first_device;
     if (cfg->device_count > 0) want = cfg->device_count;
     cflags = cfg->flags;
@@ -728,10 +835,13 @@ int stl_init(const stl_config* cfg) {
         (cflags & (STL_CFG_RCCL_GATHER | STL_CFG_NO_RCCL)) == (STL_CFG_RCCL_GATHER | STL_CFG_NO_RCCL) ||
         first < 0)
       return STL_EINVAL;
-    if (cfg->struct_size == sizeof(stl_config)) {
+    if (sz >= abi2) {
       if (cfg->reserved != 0) return STL_EINVAL;
       if (cfg->shards_per_device > 0) spd = cfg->shards_per_device;
     }
+    // registered before any device is probed: a host without a usable
+    // device still answers single calls through it
+    if (sz == sizeof(stl_config)) g_fallback_verify.store(cfg->fallback_verify);
   }
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return STL_ENODEV;
@@ -758,7 +868,10 @@ int stl_init(const stl_config* cfg) {
     const int rc = setup_device(*g_devs.back());
     if (rc) return fail(rc);
   }
-  const bool gather = !(cflags & STL_CFG_NO_RCCL) && spd == 1 && (want >= 2 || (cflags & STL_CFG_RCCL_GATHER));
+  // The in-process RCCL gather is opt-in (STL_CFG_RCCL_GATHER / STL_RCCL=1):
+  // every device copies its own slice to the host unless asked, until a
+  // multi-GPU run has shown the gathered bitmaps equal.
+  const bool gather = !(cflags & STL_CFG_NO_RCCL) && spd == 1 && (cflags & STL_CFG_RCCL_GATHER);
   if (gather) {
     if (!g_rccl.load() || fault_now()) return fail(STL_ERCCL);
     std::vector<ncclComm_t> comms(want);
@@ -808,6 +921,38 @@ const char* stl_strerror(int rc) {
 }
 
 void stl_debug_fault_after(long long calls) { g_fault_after.store(calls < 0 ? -1 : calls); }
+
+int stl_debug_tuning(int key, int value) {
+  if (value == -1) {  // query
+    switch (key) {
+      case STL_TUNE_FUSED_PREP: return g_tune_fused.load();
+      case STL_TUNE_MAIN_QUEUE: return g_tune_queue.load();
+      case STL_TUNE_STREAMS: return g_tune_streams.load();
+      case STL_TUNE_CHUNK_LOG2: return g_tune_sub_log2.load();
+      case STL_TUNE_BYTE_SHARDS: return g_tune_byte_shards.load();
+      default: return STL_EINVAL;
+    }
+  }
+  switch (key) {
+    case STL_TUNE_FUSED_PREP:
+      if (value != 0 && value != 1) return STL_EINVAL;
+      return g_tune_fused.exchange(value);
+    case STL_TUNE_MAIN_QUEUE:
+      if (value != 0 && value != 1) return STL_EINVAL;
+      return g_tune_queue.exchange(value);
+    case STL_TUNE_STREAMS:
+      if (value < 1 || value > (int)stl::kMaxVerifyStreams) return STL_EINVAL;
+      return g_tune_streams.exchange(value);
+    case STL_TUNE_CHUNK_LOG2:
+      if (value < 16 || value > 20) return STL_EINVAL;
+      return g_tune_sub_log2.exchange(value);
+    case STL_TUNE_BYTE_SHARDS:
+      if (value != 0 && value != 1) return STL_EINVAL;
+      return g_tune_byte_shards.exchange(value);
+    default:
+      return STL_EINVAL;
+  }
+}
 
 int stl_get_stats(stl_stats* out) {
   if (!out || out->struct_size != sizeof(stl_stats)) return STL_EINVAL;
@@ -924,8 +1069,33 @@ int stl_tx_blob_verify_batch(const uint8_t* blobs, const uint64_t* offset, const
                                       flags);
 }
 
+namespace {
+int verify_detached_device(const uint8_t* sig, const uint8_t* m, unsigned long long mlen, const uint8_t* pk);
+bool s_lt_l(const uint8_t* S);
+}  // namespace
+
 int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned long long mlen, const uint8_t* pk) {
   if (!sig || !pk || (mlen && !m)) return STL_EINVAL;
+  const int rc = verify_detached_device(sig, m, mlen, pk);
+  const stl_verify_fn fb = g_fallback_verify.load();
+  if (rc >= -1 || rc == STL_EINVAL || fb == nullptr) return rc;
+  // a device failure is never a reject: the caller's own check answers,
+  // composed as RippleAddress::verifySignature composes it (RippleAddress.cpp:196-199)
+  return (fb(sig, m, mlen, pk) == 0 && s_lt_l(sig + 32)) ? 0 : -1;
+}
+
+namespace {
+// crypto_sign_check_S_lt_l (RippleAddress.cpp:226-245): little-endian S < L
+bool s_lt_l(const uint8_t* S) {
+  static const uint8_t L[32] = {0xed, 0xd3, 0xf5, 0x5c, 0x1a, 0x63, 0x12, 0x58, 0xd6, 0x9c, 0xf7,
+                                0xa2, 0xde, 0xf9, 0xde, 0x14, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00,
+                                0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x10};
+  for (int i = 31; i >= 0; --i)
+    if (S[i] != L[i]) return S[i] < L[i];
+  return false;
+}
+
+int verify_detached_device(const uint8_t* sig, const uint8_t* m, unsigned long long mlen, const uint8_t* pk) {
   if (mlen == 32) {
     uint8_t bit = 0;
     const int rc = stl_ed25519_verify_batch(sig, m, pk, 1, &bit, STL_POLICY_SODIUM_1_0_18);
@@ -939,7 +1109,6 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
   Device& d = *g_devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
   STL_TRY(hipSetDevice(d.ordinal));
-  STL_RC(d.ws.ensure(stl::verify_ws_bytes(d.grid)));
   STL_RC(d.sig.ensure(64));
   STL_RC(d.pk.ensure(32));
   STL_RC(d.msg.ensure(32));
@@ -957,10 +1126,9 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
     uint64_t* meta = static_cast<uint64_t*>(d.off.p);
     STL_TRY(stl::launch_hram_var(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.pk.p),
                                  static_cast<uint8_t*>(d.pre.p), meta, meta + 1, 1, static_cast<uint8_t*>(d.msg.p), s));
-    STL_TRY(stl::launch_verify(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
-                               static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p),
-                               STL_POLICY_SODIUM_1_0_18, static_cast<uint4*>(d.ws.p), 1, true,
-                               static_cast<const uint4*>(d.wide.p), s, dev_counters(d), phase_clock(d), pair_max(d)));
+    STL_RC(run_verify(d, d.host, s, static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
+                      static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p), STL_POLICY_SODIUM_1_0_18,
+                      true, 1));
     STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
     STL_TRY(hipStreamSynchronize(s));
     return STL_OK;
@@ -970,6 +1138,7 @@ int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned l
   if (rc || drc) return rc ? rc : drc;
   return (word & 1) ? 0 : -1;
 }
+}  // namespace
 
 namespace {
 int device_for_call(Device** out) {
@@ -990,12 +1159,8 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint4* ws = nullptr;
-  STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
-  STL_TRY(stl::launch_verify(d_sig, d_msg, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             verify_grid_for(*d, n), false, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
-                             phase_clock(*d), pair_max(*d)));
-  return STL_OK;
+  return run_verify(*d, stream_ctx(*d, s), s, d_sig, d_msg, d_pk, n, d_bitmap_words, stl::kernel_mode(flags), false,
+                    g_tune_streams.load());
 }
 
 int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const uint8_t* d_pk, size_t n,
@@ -1007,12 +1172,8 @@ int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const ui
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint4* ws = nullptr;
-  STL_RC(stream_workspace(*d, s, &ws, (flags & STL_DEDUP_KEYS) != 0));
-  STL_TRY(stl::launch_verify(d_sig, d_k, d_pk, (uint32_t)n, d_bitmap_words, stl::kernel_mode(flags), ws,
-                             verify_grid_for(*d, n), true, static_cast<const uint4*>(d->wide.p), s, dev_counters(*d),
-                             phase_clock(*d), pair_max(*d)));
-  return STL_OK;
+  return run_verify(*d, stream_ctx(*d, s), s, d_sig, d_k, d_pk, n, d_bitmap_words, stl::kernel_mode(flags), true,
+                    g_tune_streams.load());
 }
 
 int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offset, const uint32_t* d_len, size_t n,
@@ -1059,9 +1220,25 @@ int stl_ed25519_sign_batch_device(const uint8_t* d_seed, const uint8_t* d_msg, s
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint4* ws = nullptr;
-  STL_RC(stream_workspace(*d, s, &ws));
-  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, ws, grid_for(*d, n), s));
+  StreamCtx& c = stream_ctx(*d, s);
+  STL_RC(c.ws[0].ensure(stl::verify_ws_bytes(d->grid)));
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws[0].p), grid_for(*d, n), s));
+  return STL_OK;
+}
+
+int stl_debug_sign_adversarial_device(const uint8_t* d_seed, const uint8_t* d_msg, const uint8_t* d_cls,
+                                      const uint32_t* d_param, size_t n, uint8_t* d_pk, uint8_t* d_sig,
+                                      uint8_t* d_msg_out, void* stream) {
+  if (n == 0) return STL_OK;
+  if (!d_seed || !d_msg || !d_cls || !d_param || !d_pk || !d_sig || !d_msg_out || n > 0xffffffc0ull)
+    return STL_EINVAL;
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  StreamCtx& c = stream_ctx(*d, s);
+  STL_RC(c.ws[0].ensure(stl::verify_ws_bytes(d->grid)));
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws[0].p), grid_for(*d, n), s,
+                           d_cls, d_param, d_msg_out));
   return STL_OK;
 }
 
@@ -1098,6 +1275,25 @@ void stl_comm_destroy(void) {
   if (g_pcomm && g_rccl.ok) (void)g_rccl.CommDestroy(g_pcomm);
   g_pcomm = nullptr;
   g_pcomm_ranks = 0;
+}
+
+int stl_comm_info(int* nranks, int* rank) {
+  if (!nranks || !rank) return STL_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(g_pcomm_mu);
+    if (g_pcomm) {
+      STL_RCCL_TRY(g_rccl.CommCount(g_pcomm, nranks));
+      STL_RCCL_TRY(g_rccl.CommUserRank(g_pcomm, rank));
+      return STL_OK;
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_comm_gather || g_devs.empty()) return STL_ERCCL;
+  int di = current_device_index();
+  if (di < 0) di = 0;
+  STL_RCCL_TRY(g_rccl.CommCount(g_devs[di]->comm, nranks));
+  STL_RCCL_TRY(g_rccl.CommUserRank(g_devs[di]->comm, rank));
+  return STL_OK;
 }
 
 int stl_bitmap_gather_device(const uint64_t* d_words, size_t words_per_rank, uint64_t* d_all_words, int root,

@@ -17,7 +17,10 @@ constexpr size_t kWsBytesPerBlock = (size_t)kBlock * kSlotQuads * 16;
 // of kPreChunk signatures (a multiple of 64, so chunks start on bitmap words),
 // plus one fallback-flag word per 64 signatures
 constexpr uint32_t kPreChunk = 1u << 20;
-constexpr size_t kPreBytes = (size_t)kPreChunk * 224 + (size_t)kPreChunk / 8;
+// work counters of the main kernel's unit queue, one per chunk a launch_verify
+// call runs on a workspace (chunks >= 2^16 signatures, n < 2^32)
+constexpr uint32_t kMainQueueWords = 1u << 16;
+constexpr size_t kPreBytes = (size_t)kPreChunk * 224 + (size_t)kPreChunk / 8 + (size_t)kMainQueueWords * 4;
 // Per-batch key dedup (STL_DEDUP_KEYS), per kPreChunk signatures: an open-
 // addressing table of 2 * kPreChunk slots, representative / unique-id /
 // owner arrays, a counter, and the decoded keys (-A affine + ok, 5 x uint4).
@@ -42,10 +45,15 @@ inline size_t verify_ws_bytes(uint32_t grid, bool dedup = false) {
 constexpr uint32_t kModeFullLength = 0x100u;
 constexpr uint32_t kModeDedupKeys = 0x200u;
 constexpr uint32_t kModeOneLane = 0x400u;
+// bit 11 = the raw predicate without stellard's S < L (STL_DEBUG_RAW_PREDICATE, test-only)
+constexpr uint32_t kModeRaw = 0x800u;
 inline uint32_t kernel_mode(uint32_t flags) {
   return (flags & 0x1u) | ((flags & 0x4u) ? kModeFullLength : 0u) | ((flags & 0x8u) ? kModeDedupKeys : 0u) |
-         ((flags & 0x10u) ? kModeOneLane : 0u);
+         ((flags & 0x10u) ? kModeOneLane : 0u) | ((flags & 0x80000000u) ? kModeRaw : 0u);
 }
+// the policy argument of the verify core (stl_verify_core.h): bit 0 the
+// libsodium policy, bit 1 (kPolicyRaw) the raw predicate
+__host__ __device__ inline uint32_t core_policy(uint32_t mode) { return (mode & 1u) | ((mode & kModeRaw) ? 2u : 0u); }
 
 const void* kernel_verify_msg32();
 // counters (nullable): device u64 [0] accept bits written, [1] lanes checked by
@@ -57,15 +65,38 @@ const void* kernel_verify_msg32();
 // shorter chains save.
 // Optional phase clock (stl_set_phase_timing): launch_verify calls
 // mark(ctx, stream, i) before a chunk's first kernel (i = 0) and after each
-// phase -- 1 scalar, 2 point (+ the key-dedup kernels), 3 main, 4 fallback.
+// phase -- 1 scalar (the whole of phase 1 when it runs as one kernel), 2 point
+// (+ the key-dedup kernels), 3 main, 4 fallback.
 struct PhaseClock {
   void (*mark)(void* ctx, hipStream_t stream, int i);
   void* ctx;
 };
+// How launch_verify runs a batch.  The batch is cut into chunks (at most
+// kPreChunk signatures, the phase-1 state a workspace holds); each chunk is
+// phase 1, main, fallback on one stream.  With nstreams > 1 (and no phase
+// clock, whose per-kernel durations need kernels that do not overlap) chunk i
+// of `sub` signatures runs on streams[i % nstreams] with workspace
+// ws[i % nstreams]: the streams fork from streams[0] (the caller's) through
+// `fork` and join it through `join`, so one chunk's phase-1 kernels and the
+// next chunks' kernels fill the ragged last rounds of each other's launches.
+constexpr uint32_t kMaxVerifyStreams = 4;
+struct VerifyExec {
+  uint32_t grid = 1;                    // resident workgroups = per-lane workspace slots per ws
+  uint32_t pair_max = 0;                // chunks up to this size run two lanes per signature
+  const uint4* wide = nullptr;          // wide base tables
+  unsigned long long* counters = nullptr;
+  const PhaseClock* clock = nullptr;
+  bool fused_prep = true;               // scalar + point half of phase 1 in one kernel
+  bool main_queue = true;               // main kernel pulls 64-signature units from a counter
+  uint32_t nstreams = 1;
+  uint32_t sub = kPreChunk;             // chunk size when nstreams > 1 (multiple of 64, >= 2^16)
+  hipStream_t streams[kMaxVerifyStreams] = {};
+  uint4* ws[kMaxVerifyStreams] = {};    // verify_ws_bytes(grid, dedup) each
+  hipEvent_t fork = nullptr;
+  hipEvent_t join[kMaxVerifyStreams] = {};
+};
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
-                         uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k, const uint4* wide,
-                         hipStream_t stream, unsigned long long* counters = nullptr,
-                         const PhaseClock* clock = nullptr, uint32_t pair_max = 0);
+                         uint64_t* bitmap, uint32_t policy, bool pre_k, const VerifyExec& x);
 hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t* m, const uint64_t* moff,
                            const uint64_t* mlen, uint32_t n, uint8_t* k_out, hipStream_t stream);
 // counter: one device word of scratch (reset by the launcher); grid: upper
@@ -82,7 +113,10 @@ hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint3
 // Wide base tables (stl_verify_core.h): 2 * 32769 rows of 28 words.
 constexpr size_t kWideTableBytes = 2ull * 32769 * 28 * 4;
 hipError_t launch_wide_table(uint4* out, hipStream_t stream);
+// cls / param (nullable, test data only): per-row adversarial class and its
+// parameter (stl_kernels.hip adversarial_row); msg_out receives the messages.
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
-                       uint32_t grid, hipStream_t stream);
+                       uint32_t grid, hipStream_t stream, const uint8_t* cls = nullptr,
+                       const uint32_t* param = nullptr, uint8_t* msg_out = nullptr);
 
 }  // namespace stl

@@ -205,12 +205,45 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_point_k
   const uint4 q2 = q[kHalfTopsWord / 4];
   w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
   static_assert(kHalfTopsWord == 10, "tops is word 2 of quad 2");
-  verify_phase1_points(h, R, S, A, policy & 1u);
+  verify_phase1_points(h, R, S, A, core_policy(policy));
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
   if (live) {
     st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
 #pragma unroll
     for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+  }
+  const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
+  if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
+}
+
+// Phase 1 in one launch (the default for chunks that run one lane per
+// signature without key dedup): the scalar half, then the point half, in the
+// same lane.  The two halves' state never leaves the registers between them,
+// and the chunk pays one kernel boundary instead of two -- the scalar
+// kernel alone ends in a ragged last round (3.2 rounds of 5 workgroups per
+// CU for 2^20 signatures).
+template <bool PRE_K>
+__global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_prep_kernel(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
+    uint32_t base, uint32_t cnt, uint32_t policy, uint4* __restrict__ pre, uint64_t* __restrict__ fb_words) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = t < cnt;
+  const uint32_t tt = live ? t : cnt - 1;
+  const size_t j = (size_t)base + tt;
+  uint32_t R[8], S[8], A[8], k[8];
+  ld8(R, sig + 64 * j);
+  ld8(S, sig + 64 * j + 32);
+  ld8(A, pk + 32 * j);
+  load_k(k, R, A, msg_or_k, j, PRE_K);
+  HalfState h;
+  verify_phase1_scalars(h, S, k);
+  verify_phase1_points(h, R, S, A, core_policy(policy));
+  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  if (live) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
+    uint4* q = pre + (size_t)t * 14;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
   }
   const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
@@ -249,9 +282,9 @@ __global__ __launch_bounds__(kBlock, 2) void verify_point_pair_kernel(
   }
   const bool ook = __shfl_xor((int)mok, 1) != 0;
   if (par == 0)
-    phase1_points_finish_pair(h, R, S, A, policy & 1u, mx, my, mok, ox, oy, ook);
+    phase1_points_finish_pair(h, R, S, A, core_policy(policy), mx, my, mok, ox, oy, ook);
   else
-    phase1_points_finish_pair(h, R, S, A, policy & 1u, ox, oy, ook, mx, my, mok);
+    phase1_points_finish_pair(h, R, S, A, core_policy(policy), ox, oy, ook, mx, my, mok);
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
   if (live && par == 0) {
     st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
@@ -455,7 +488,7 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
   w[16] = q4.x; w[17] = q4.y; w[18] = q4.z;
   const uint32_t c_neg = h.tops & kHalfCNeg;
-  verify_phase1_points_keyed(h, R, S, A, policy & 1u, nAx, nAy, kw[18] != 0);
+  verify_phase1_points_keyed(h, R, S, A, core_policy(policy), nAx, nAy, kw[18] != 0);
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
   h.pad = uid;
   const uint32_t nu = *counter;
@@ -561,9 +594,14 @@ struct WideGlobal {
   }
 };
 
-// Phase 2: [e]B + [c](-A) + [d](-Q) == O; grid-strides over 256-signature
-// tiles of [base, base+cnt) so the per-lane table workspace is bounded by the
-// resident lanes; one ballot word per wave.
+// Phase 2: [e]B + [c](-A) + [d](-Q) == O over [base, base+cnt); one ballot
+// word per wave.  The grid is the resident capacity (the per-lane table
+// workspace is bounded by the resident lanes).  Work unit = 64 signatures
+// (one wave, one bitmap word): with `queue` each wave pulls its next unit from
+// that counter (zeroed by the launcher), so waves that finish early take more
+// and the kernel's last round is not fixed in advance; without it the units
+// are dealt out statically (grid stride).  Every wave leaves after one pull
+// past the end.
 #ifdef STL_MAIN_NUM_VGPR
 #define STL_MAIN_ATTR __attribute__((amdgpu_num_vgpr(STL_MAIN_NUM_VGPR)))
 #else
@@ -572,7 +610,7 @@ struct WideGlobal {
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
     uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
-    const uint4* __restrict__ keytabs, const uint4* __restrict__ widetabs) {
+    const uint4* __restrict__ keytabs, const uint4* __restrict__ widetabs, uint32_t* __restrict__ queue) {
   TableView tab1, tab2;
   lane_tables(ws, tab1, tab2);
 #ifndef STL_TAILS_GLOBAL
@@ -594,18 +632,28 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
   __shared__ uint4 wstage[kBlock / 64][2 * kWideQuads * 64];
   WideLds wl{wide, wstage[wave], lane, {0, 0}};
 #endif
-  for (uint32_t tile = blockIdx.x * kBlock; tile < cnt; tile += gridDim.x * kBlock) {
-    const uint32_t t = tile + threadIdx.x;
+  const uint32_t units = (cnt + 63) >> 6;
+  const uint32_t stride = gridDim.x * (kBlock / 64);
+  uint32_t unit = blockIdx.x * (kBlock / 64) + wave;
+  for (;;) {
+    if (queue) {  // wave-uniform: one atomic per wave and unit
+      uint32_t u = 0;
+      if (lane == 0) u = atomicAdd(queue, 1u);
+      unit = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+    }
+    if (unit >= units) break;
+    const uint32_t wbase = unit * 64;
+    const uint32_t t = wbase + lane;
     const bool live = t < cnt;
     HalfState h;
     ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
     const bool ok = verify_phase2_half(h, tab1, tab2, wl, keytabs, widetabs) && live;
     const uint64_t word = __ballot(ok);
-    const uint32_t wbase = tile + wave * 64;
-    if (lane == 0 && wbase < cnt) {
+    if (lane == 0) {
       bitmap[(base + wbase) >> 6] = word;
       if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popcll(word));  // accepted (stl_get_stats)
     }
+    if (!queue) unit += stride;
   }
 }
 
@@ -687,7 +735,7 @@ __global__ __launch_bounds__(kBlock, 2) void verify_fallback_kernel(
       ld8(S, sig + 64 * j + 32);
       ld8(A, pk + 32 * j);
       load_k(k, R, A, msg_or_k, j, PRE_K);
-      ok = verify_full_with_k(R, S, A, k, policy & 1u, tab, sB);
+      ok = verify_full_with_k(R, S, A, k, core_policy(policy), tab, sB);
     }
     const uint64_t word = __ballot(ok);
     if (lane == 0) {
@@ -1031,10 +1079,185 @@ __device__ __forceinline__ void sha512_short(uint32_t out[16], const uint32_t* i
   sha512_digest_le32(out, st);
 }
 
+// ---- adversarial rows of the full-size parity datasets (test data only) ----
+// SURVEY.md Appendix B classes, each built from a row's own honest signature
+// (tests/datasets.py holds the same construction on the host, over libsodium;
+// the input digests of the committed datasets pin the two against each other).
+// u is the row's 32-bit parameter.
+//   1 B1   msg byte u%32 ^= 1 << ((u>>5)&7)
+//   2 B2   R   byte u%32 ^= 1 << ((u>>5)&7)
+//   3 B3   clear the first set bit of S at or below bit u%252, scanning down
+//          (wrapping from 0 to 251): S stays < L
+//   4 B4   S += L
+//   5 B5   sig[63] |= {0xE0, 0x80, 0x40, 0x20}[u%4] (S >= 2^253)
+//   6 B6   pk = kSmallOrderEnc[u%14], R = encode([S]B)
+//   7 B7   R = kSmallOrderEnc[u%14], S = k*a mod L, k = H(R||A||M) mod L
+//   8 B8   pk = A' = A + kTorsionEnc[1 + u%7], S = r + k*a, k = H(R||A'||M)
+//   9 B9   pk = p + 2 + u%17 (non-canonical y), sign bit (u>>8)&1
+//  10 B10  pk = y + j | sign, the first j in 1..64 with y + j < p not on the curve
+//  11 B11  u even: R's sign bit flipped; u odd: R = kNonCanonR[(u>>1)%3], S = k*a
+__constant__ uint32_t kSmallOrderEnc[14][8] = {
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
+    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
+    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
+    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x85fc536du},
+    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
+    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0xfa03ac92u},
+    {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+    {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu},
+    {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+    {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu},
+    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu}};
+// i * T8, i = 0..7 (T8 = the order-8 point encoded 26e8...05)
+__constant__ uint32_t kTorsionEnc[8][8] = {
+    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
+    {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0xfa03ac92u},
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
+    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x85fc536du}};
+// non-canonical encodings of the identity: y = p + 1; y = 1 with the sign bit; both
+__constant__ uint32_t kNonCanonR[3][8] = {
+    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
+    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu}};
+
+__device__ __forceinline__ void copy8(uint32_t d[8], const uint32_t s[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d[i] = s[i];
+}
+
+// x (8 words) += y (8 words), mod 2^256
+__device__ __forceinline__ void add256(uint32_t x[8], const uint32_t y[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)x[i] + y[i];
+    x[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
+// Mutates one honest row (A, R, S, M; a the clamped secret scalar, r the
+// nonce) into class `c` with parameter u (table above).
+__device__ void adversarial_row(uint32_t c, uint32_t u, uint32_t A[8], uint32_t R[8], uint32_t S[8], uint32_t M[8],
+                                const uint32_t a[8], const uint32_t r[8], const TableView& tv, const uint32_t* sB) {
+  const uint32_t byte = u % 32u, bit = 1u << ((u >> 5) & 7u);
+  uint32_t zero[8], k[8], h[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) zero[i] = 0;
+  switch (c) {
+    case 1: M[byte >> 2] ^= bit << (8 * (byte & 3u)); break;
+    case 2: R[byte >> 2] ^= bit << (8 * (byte & 3u)); break;
+    case 3: {
+      const uint32_t b0 = u % 252u;
+      for (uint32_t s = 0; s < 252u; ++s) {
+        const uint32_t b = (b0 + 252u - s) % 252u;
+        if ((S[b >> 5] >> (b & 31u)) & 1u) {
+          S[b >> 5] &= ~(1u << (b & 31u));
+          break;
+        }
+      }
+      break;
+    }
+    case 4: {
+      uint32_t Lw[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) Lw[i] = sc_L(i);
+      add256(S, Lw);
+      break;
+    }
+    case 5: {
+      const uint32_t pat[4] = {0xE0u, 0x80u, 0x40u, 0x20u};
+      S[7] |= pat[u % 4u] << 24;
+      break;
+    }
+    case 6: {
+      copy8(A, kSmallOrderEnc[u % 14u]);
+      ge_p3 id;
+      ge_p3_0(id);
+      ge_p2 P;
+      double_scalarmult(P, id, zero, S, tv, sB);  // [S]B
+      ge_tobytes(R, P);
+      break;
+    }
+    case 7:
+    case 11: {
+      if (c == 11 && (u & 1u) == 0) {
+        R[7] ^= 0x80000000u;
+        break;
+      }
+      copy8(R, c == 7 ? kSmallOrderEnc[u % 14u] : kNonCanonR[(u >> 1) % 3u]);
+      sha512_hram32(h, R, A, M);
+      sc_reduce64(k, h);
+      sc_muladd(S, k, a, zero);  // [S]B - [k]A = O
+      break;
+    }
+    case 8: {
+      ge_p3 nA, nT;
+      uint32_t T[8];
+      copy8(T, kTorsionEnc[1u + u % 7u]);
+      ge_frombytes_negate_vartime(nA, A);
+      ge_frombytes_negate_vartime(nT, T);
+      ge_cached cT;
+      ge_p3_to_cached(cT, nT);
+      ge_p1p1 t;
+      ge_add_cached(t, nA, cT);  // -(A + T)
+      ge_p2 s;
+      ge_p1p1_to_p2(s, t);
+      fe_neg(s.X, s.X);
+      ge_tobytes(A, s);
+      sha512_hram32(h, R, A, M);
+      sc_reduce64(k, h);
+      sc_muladd(S, k, a, r);
+      break;
+    }
+    case 9: {
+      const uint32_t j = 2u + u % 17u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) A[i] = i == 0 ? 0xffffffedu + j : (i == 7 ? 0x7fffffffu : 0xffffffffu);
+      A[7] |= ((u >> 8) & 1u) << 31;
+      break;
+    }
+    case 10: {
+      const uint32_t sign = A[7] & 0x80000000u;
+      uint32_t y[8];
+      copy8(y, A);
+      y[7] &= 0x7fffffffu;
+      for (uint32_t j = 1; j <= 64u; ++j) {
+        uint32_t one[8] = {1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        add256(y, one);
+        if (!point_is_canonical(y) || (y[7] >> 31) != 0) continue;
+        uint32_t cand[8];
+        copy8(cand, y);
+        cand[7] |= sign;
+        ge_p3 tmp;
+        if (!ge_frombytes_negate_vartime(tmp, cand)) {
+          copy8(A, cand);
+          break;
+        }
+      }
+      break;
+    }
+    default: break;
+  }
+}
+
+// RFC 8032 keypair + signature per row; with `cls` (test data only) rows
+// whose class is not 0 are then mutated by adversarial_row and msg_out gets
+// the (possibly mutated) message.
+template <bool ADV>
 __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restrict__ seed,
                                                       const uint8_t* __restrict__ msg, uint32_t n,
                                                       uint8_t* __restrict__ pk_out, uint8_t* __restrict__ sig_out,
-                                                      uint4* __restrict__ ws) {
+                                                      uint4* __restrict__ ws, const uint8_t* __restrict__ cls,
+                                                      const uint32_t* __restrict__ param,
+                                                      uint8_t* __restrict__ msg_out) {
   __shared__ uint32_t sB[kBaseTableWords];
   stage_base_table(sB, 1);
   TableView tv, unused;
@@ -1079,10 +1302,15 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
     sha512_hram32(kh, R, A, M);
     sc_reduce64(k, kh);
     sc_muladd(S, k, a, r);                                   // S = r + k a mod L
+    if (ADV) {
+      const uint32_t c = cls[j];
+      if (c != 0) adversarial_row(c, param[j], A, R, S, M, a, r, tv, sB);
+    }
     if (live) {
       st8(pk_out + 32 * j, A);
       st8(sig_out + 64 * j, R);
       st8(sig_out + 64 * j + 32, S);
+      if (ADV) st8(msg_out + 32 * j, M);
     }
   }
 }
@@ -1121,15 +1349,19 @@ hipError_t launch_wide_table(uint4* out, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
-                         uint64_t* bitmap, uint32_t policy, uint4* ws, uint32_t grid, bool pre_k,
-                         const uint4* wide, hipStream_t stream, unsigned long long* counters,
-                         const PhaseClock* clock, uint32_t pair_max) {
-  if (n == 0) return hipSuccess;
+// One chunk (<= kPreChunk signatures at [base, base+cnt)) on one stream and
+// workspace: phase 1, main, fallback.  `qctr` is the chunk's zeroed counter
+// of the main kernel's unit queue.
+static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t base,
+                               uint32_t cnt, uint64_t* bitmap, uint32_t policy, bool pre_k, const VerifyExec& x,
+                               hipStream_t stream, uint4* ws, uint32_t* qctr, const PhaseClock* clock) {
+  const uint32_t grid = x.grid, pair_max = x.pair_max;
+  const uint4* wide = x.wide;
+  unsigned long long* counters = x.counters;
   auto mark = [&](int i) {
     if (clock) clock->mark(clock->ctx, stream, i);
   };
-  // ws = [per-lane slots: grid x kWsBytesPerBlock][HalfState x kPreChunk][fallback words]
+  // ws = [per-lane slots: grid x kWsBytesPerBlock][HalfState x kPreChunk][fallback words][queue counters]
   //      [dedup (kModeDedupKeys): slots, rep, uid_of, owners, counter, decoded keys]
   uint4* slots = ws;
   uint4* pre = ws + (size_t)grid * (kWsBytesPerBlock / 16);
@@ -1144,12 +1376,11 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   uint4* keytab = reinterpret_cast<uint4*>(counter + 64);
   uint4* keytabs = keytab + (size_t)kPreChunk * 5;
   uint4* widetabs = keytabs + (size_t)kKeyTables * kTableQuadsPerKey;
-  for (uint64_t b64 = 0; b64 < n; b64 += kPreChunk) {  // 64-bit: n may reach 2^32 - 64
-    const uint32_t base = (uint32_t)b64;
-    const uint32_t cnt = n - base < kPreChunk ? n - base : kPreChunk;
+  {
     const dim3 g1((cnt + kBlock - 1) / kBlock);
-    const uint32_t tiles = (cnt + kBlock - 1) / kBlock;
-    const dim3 g2(tiles < grid ? tiles : grid);
+    const uint32_t units = (cnt + 63) / 64;
+    const uint32_t wgs = (units + kBlock / 64 - 1) / (kBlock / 64);
+    const dim3 g2(wgs < grid ? wgs : grid);
     // Small chunks: two lanes per signature in the point and main kernels
     // (verify_point_pair_kernel, verify_main_pair_kernel); the bits are the
     // same.  It also takes precedence over key dedup: a chunk this small is
@@ -1165,13 +1396,22 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
 #endif
     const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
+    const bool fused = x.fused_prep && !pair_point && !dedup;
     mark(0);
-    if (pre_k)
+    if (fused && pre_k)
+      hipLaunchKernelGGL(verify_prep_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
+                         pre, fb);
+    else if (fused)
+      hipLaunchKernelGGL(verify_prep_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
+                         pre, fb);
+    else if (pre_k)
       hipLaunchKernelGGL(verify_scalar_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     else
       hipLaunchKernelGGL(verify_scalar_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     mark(1);
-    if (pair_point) {
+    if (fused) {
+      // phase 1 done
+    } else if (pair_point) {
       hipLaunchKernelGGL(verify_point_pair_kernel, gp, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     } else if (dedup) {
       uint32_t nslots = 64;
@@ -1199,7 +1439,7 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
                          counters);
     else
       hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
-                         counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr);
+                         counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr, qctr);
     mark(3);
     if (pre_k)
       hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
@@ -1208,6 +1448,56 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
       hipLaunchKernelGGL(verify_fallback_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
                          policy, fb, bitmap, slots, counters);
     mark(4);
+  }
+  return hipGetLastError();
+}
+
+// queue counters of workspace ws (after the fallback words)
+static uint32_t* queue_counters(uint4* ws, uint32_t grid) {
+  uint4* pre = ws + (size_t)grid * (kWsBytesPerBlock / 16);
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(pre + (size_t)kPreChunk * 14) + kPreChunk / 64);
+}
+
+hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
+                         uint64_t* bitmap, uint32_t policy, bool pre_k, const VerifyExec& x) {
+  if (n == 0) return hipSuccess;
+  // chunks over concurrent streams only where each stream gets whole chunks
+  // larger than the lane-pair size, and never under the phase clock
+  uint32_t S = x.nstreams < kMaxVerifyStreams ? x.nstreams : kMaxVerifyStreams;
+  const uint32_t sub = x.sub;
+  if (S > 1 && (x.clock != nullptr || sub < (1u << 16) || sub > kPreChunk || (sub & 63u) != 0 || sub <= x.pair_max ||
+                n <= sub))
+    S = 1;
+  const uint32_t csize = S > 1 ? sub : kPreChunk;
+  const uint64_t nchunks = ((uint64_t)n + csize - 1) / csize;
+  if (S > (uint32_t)nchunks) S = (uint32_t)nchunks;
+  hipError_t e;
+  if (S > 1) {
+    if ((e = hipEventRecord(x.fork, x.streams[0])) != hipSuccess) return e;
+    for (uint32_t j = 1; j < S; ++j)
+      if ((e = hipStreamWaitEvent(x.streams[j], x.fork, 0)) != hipSuccess) return e;
+  }
+  if (x.main_queue) {  // zero each stream's counters: one per chunk it runs
+    for (uint32_t j = 0; j < S; ++j) {
+      const uint64_t cj = (nchunks - j + S - 1) / S;
+      e = hipMemsetAsync(queue_counters(x.ws[j], x.grid), 0, cj * 4, x.streams[j]);
+      if (e != hipSuccess) return e;
+    }
+  }
+  for (uint64_t c = 0; c < nchunks; ++c) {  // 64-bit: n may reach 2^32 - 64
+    const uint32_t j = (uint32_t)(c % S);
+    const uint32_t base = (uint32_t)(c * csize);
+    const uint32_t cnt = n - base < csize ? n - base : csize;
+    uint32_t* q = x.main_queue ? queue_counters(x.ws[j], x.grid) + c / S : nullptr;
+    e = verify_chunk(sig, msg_or_k, pk, base, cnt, bitmap, policy, pre_k, x, x.streams[j], x.ws[j], q,
+                     S > 1 ? nullptr : x.clock);
+    if (e != hipSuccess) return e;
+  }
+  if (S > 1) {
+    for (uint32_t j = 1; j < S; ++j) {
+      if ((e = hipEventRecord(x.join[j], x.streams[j])) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(x.streams[0], x.join[j], 0)) != hipSuccess) return e;
+    }
   }
   return hipGetLastError();
 }
@@ -1260,9 +1550,15 @@ hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint3
 }
 
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
-                       uint32_t grid, hipStream_t stream) {
+                       uint32_t grid, hipStream_t stream, const uint8_t* cls, const uint32_t* param,
+                       uint8_t* msg_out) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(sign_kernel, dim3(grid), dim3(kBlock), 0, stream, seed, msg, n, pk, sig, ws);
+  if (cls)
+    hipLaunchKernelGGL(sign_kernel<true>, dim3(grid), dim3(kBlock), 0, stream, seed, msg, n, pk, sig, ws, cls, param,
+                       msg_out);
+  else
+    hipLaunchKernelGGL(sign_kernel<false>, dim3(grid), dim3(kBlock), 0, stream, seed, msg, n, pk, sig, ws, nullptr,
+                       nullptr, nullptr);
   return hipGetLastError();
 }
 

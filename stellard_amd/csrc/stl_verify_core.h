@@ -29,7 +29,14 @@ namespace stl {
 enum : uint32_t {
   kPolicySodium1018 = 0u,
   kPolicyStellard100 = 1u,
+  // or-ed into a policy: the raw crypto_sign_verify_detached predicate,
+  // without stellard's S < L (test-only: RippleAddress.cpp:838-845's raw
+  // expectation; STL_DEBUG_RAW_PREDICATE)
+  kPolicyRaw = 2u,
 };
+
+// stellard's composite accept needs S < L unless the raw predicate is asked for
+STL_HD bool composite_s_ok(const uint32_t S[8], uint32_t policy) { return (policy & kPolicyRaw) != 0 || sc_lt_L(S); }
 
 STL_HD uint32_t small_order_word(int e, int i) {
   const uint32_t bl[7][8] = {
@@ -77,7 +84,7 @@ STL_HD bool all_zero(const uint32_t s[8]) {
 // case is parity-unpinned offline and a reject is the
 // safe side: stellard then runs its own serial check.
 STL_HD bool verify_prechecks(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], uint32_t policy) {
-  if (policy == kPolicyStellard100) return (S[7] >> 29) == 0 && !all_zero(A);  // sig[63] & 224
+  if ((policy & 1u) == kPolicyStellard100) return (S[7] >> 29) == 0 && !all_zero(A);  // sig[63] & 224
   return sc_lt_L(S) && !has_small_order(R) && point_is_canonical(A) && !has_small_order(A);
 }
 
@@ -288,7 +295,7 @@ STL_HD void verify_phase1(PreState& o, const uint32_t R[8], const uint32_t S[8],
   ge_p3 negA;
   ok = ge_frombytes_negate_vartime(negA, A) && ok;
   // stellard composite: && signatureIsCanonical (S < L), RippleAddress.cpp:198-199
-  ok = ok && sc_lt_L(S);
+  ok = ok && composite_s_ok(S, policy);
 #pragma unroll
   for (int i = 0; i < 8; ++i) o.k[i] = k[i];
   o.negAx = negA.X;
@@ -418,7 +425,7 @@ STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32
                                  uint32_t policy) {
   bool ok = verify_prechecks(R, S, A, policy);
   // stellard composite: && signatureIsCanonical (S < L), RippleAddress.cpp:198-199
-  ok = ok && sc_lt_L(S) && r_is_canonical(R);  // before the decodings: R, S not live across them
+  ok = ok && composite_s_ok(S, policy) && r_is_canonical(R);  // before the decodings: R, S not live across them
   ge_p3 negA, negQ;
   bool okA, okR;
 #ifndef STL_POINT_PAIRED
@@ -451,7 +458,7 @@ STL_HD void phase1_points_finish_pair(HalfState& o, const uint32_t R[8], const u
                                       uint32_t policy, const fe& nAx, const fe& nAy, bool okA, const fe& nQx,
                                       const fe& nQy, bool okR) {
   bool ok = verify_prechecks(R, S, A, policy);
-  ok = ok && sc_lt_L(S) && r_is_canonical(R) && okA && okR;
+  ok = ok && composite_s_ok(S, policy) && r_is_canonical(R) && okA && okR;
   finish_phase1_points(o, nAx, nAy, nQx, nQy, ok);
 }
 
@@ -462,7 +469,7 @@ STL_HD void phase1_points_finish_pair(HalfState& o, const uint32_t R[8], const u
 STL_HD void verify_phase1_points_keyed(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
                                        uint32_t policy, const fe& negAx, const fe& negAy, bool okA) {
   bool ok = verify_prechecks(R, S, A, policy);
-  ok = ok && sc_lt_L(S) && r_is_canonical(R);
+  ok = ok && composite_s_ok(S, policy) && r_is_canonical(R);
   ge_p3 negQ;
   const bool okR = ge_frombytes_negate_vartime(negQ, R);
   ok = ok && okA && okR;
@@ -710,8 +717,8 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
   return (p.tops & kHalfOk) != 0 && (p.tops & kHalfFallback) == 0 && id;
 }
 
-// Small batches (fewer signatures than half the resident lanes): one
-// signature on two lanes.  Lane `par` = 0 runs [e_lo]B + [c]P1 (the low
+// Small batches (at most a quarter of the resident lanes, launch_verify's
+// pair_max: one pair wave per SIMD): one signature on two lanes.  Lane `par` = 0 runs [e_lo]B + [c]P1 (the low
 // wide table), lane 1 runs [e_hi]2^128 B + [d]P2 (the high one), on the same
 // doubling schedule as verify_phase2_half -- one table, one add per position
 // and one madd per fourth position instead of two each.  The pair then checks

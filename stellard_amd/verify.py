@@ -36,17 +36,30 @@ def _buf(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+# libsodium's crypto_sign_verify_detached signature (stl_verify_fn)
+VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulonglong, ctypes.c_void_p)
+
+
 class Config(ctypes.Structure):
-    """stl_config (include/stl.h, ABI 2)."""
+    """stl_config (include/stl.h, ABI 3)."""
     _fields_ = [("struct_size", ctypes.c_uint32), ("device_count", ctypes.c_int32),
                 ("first_device", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("shards_per_device", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+                ("shards_per_device", ctypes.c_int32), ("reserved", ctypes.c_uint32),
+                ("fallback_verify", VERIFY_FN)]
 
 
-def init(device_count=0, first_device=0, flags=0, shards_per_device=1):
+_fallback_keepalive = []
+
+
+def init(device_count=0, first_device=0, flags=0, shards_per_device=1, fallback_verify=None):
     """stl_init (sodium_init's place, ripple_app.cpp:129-132).  flags:
-    N.STL_CFG_RCCL_GATHER / N.STL_CFG_NO_RCCL."""
-    cfg = Config(ctypes.sizeof(Config), device_count, first_device, flags, shards_per_device, 0)
+    N.STL_CFG_RCCL_GATHER / N.STL_CFG_NO_RCCL.  ``fallback_verify``: a
+    VERIFY_FN (the caller's libsodium check) that stl_ed25519_verify_detached
+    answers device failures with."""
+    fb = fallback_verify if fallback_verify is not None else VERIFY_FN()
+    if fallback_verify is not None:
+        _fallback_keepalive.append(fallback_verify)  # libstl keeps the pointer
+    cfg = Config(ctypes.sizeof(Config), device_count, first_device, flags, shards_per_device, 0, fb)
     return N.check(N.load().stl_init(ctypes.byref(cfg)), "stl_init")
 
 
@@ -426,6 +439,14 @@ def comm_destroy():
     N.load().stl_comm_destroy()
 
 
+def comm_info():
+    """stl_comm_info: (nranks, rank) as RCCL reports them (ncclCommCount /
+    ncclCommUserRank) for the communicator libstl gathers over."""
+    nr, r = ctypes.c_int(0), ctypes.c_int(0)
+    N.check(N.load().stl_comm_info(ctypes.byref(nr), ctypes.byref(r)), "stl_comm_info")
+    return nr.value, r.value
+
+
 def bitmap_gather_device(words, out_words=None, root=0, stream=None):
     """stl_bitmap_gather_device: every rank's int64 bitmap words (CUDA tensor of
     words_per_rank words) into out_words (nranks*words_per_rank) on rank
@@ -446,7 +467,11 @@ class Stats(ctypes.Structure):
                 ("phase_ns", ctypes.c_uint64 * 4), ("phase_chunks", ctypes.c_uint64)]
 
 
-PHASES = ("scalar", "point", "main", "fallback")
+# stl_stats.phase_ns: [0] the first phase-1 kernel -- all of phase 1 when it
+# runs as one kernel (the default), the SHA-512 + lattice kernel when split;
+# [1] the point-decoding kernel when split, the key-dedup kernels; [2] the main
+# kernel; [3] the full-length fallback kernel
+PHASES = ("phase1", "point", "main", "fallback")
 
 
 def get_stats():
@@ -490,6 +515,28 @@ def debug_verify_k_device(sig, k, pk, out_words=None, policy=POLICY_SODIUM_1_0_1
     return out_words
 
 
+TUNE_FUSED_PREP, TUNE_MAIN_QUEUE = N.STL_TUNE_FUSED_PREP, N.STL_TUNE_MAIN_QUEUE
+TUNE_STREAMS, TUNE_CHUNK_LOG2 = N.STL_TUNE_STREAMS, N.STL_TUNE_CHUNK_LOG2
+TUNE_BYTE_SHARDS = N.STL_TUNE_BYTE_SHARDS
+
+
+def debug_tuning(key, value):
+    """stl_debug_tuning: process-wide execution setting (same accept bits
+    whatever the value); returns the previous value."""
+    rc = N.load().stl_debug_tuning(key, value)
+    if rc < 0:
+        raise N.StlError(rc, "stl_debug_tuning")
+    return rc
+
+
+def execution_settings():
+    """The current stl_debug_tuning values."""
+    lib = N.load()
+    return {name: lib.stl_debug_tuning(key, -1) for name, key in (
+        ("fused_prep", TUNE_FUSED_PREP), ("main_queue", TUNE_MAIN_QUEUE), ("streams", TUNE_STREAMS),
+        ("chunk_log2", TUNE_CHUNK_LOG2))}
+
+
 def sign_batch_device(seed, msg, stream=None):
     """RFC 8032 keypair(seed) + detached signature over msg, on the GPU.
     seed (n,32), msg (n,32) uint8 CUDA tensors -> (pk (n,32), sig (n,64))."""
@@ -501,6 +548,25 @@ def sign_batch_device(seed, msg, stream=None):
         ctypes.c_void_p(seed.data_ptr()), ctypes.c_void_p(msg.data_ptr()), n, ctypes.c_void_p(pk.data_ptr()),
         ctypes.c_void_p(sig.data_ptr()), _stream_ptr(stream)), "stl_ed25519_sign_batch_device")
     return pk, sig
+
+
+def sign_adversarial_device(seed, msg, cls, param, stream=None):
+    """Test data: sign_batch_device, then rows with cls (n,) uint8 in 1..11
+    mutated into SURVEY Appendix-B class B<cls> with parameter param (n,)
+    int32 (tests/datasets.py).  -> (pk, sig, msg) CUDA tensors."""
+    import torch
+    n = seed.shape[0]
+    pk = torch.empty((n, 32), dtype=torch.uint8, device=seed.device)
+    sig = torch.empty((n, 64), dtype=torch.uint8, device=seed.device)
+    mo = torch.empty((n, 32), dtype=torch.uint8, device=seed.device)
+    for t in (seed, msg, cls, param):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("device entry point needs contiguous CUDA tensors")
+    N.check(N.load().stl_debug_sign_adversarial_device(
+        ctypes.c_void_p(seed.data_ptr()), ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(cls.data_ptr()),
+        ctypes.c_void_p(param.data_ptr()), n, ctypes.c_void_p(pk.data_ptr()), ctypes.c_void_p(sig.data_ptr()),
+        ctypes.c_void_p(mo.data_ptr()), _stream_ptr(stream)), "stl_debug_sign_adversarial_device")
+    return pk, sig, mo
 
 
 def words_to_bool(words, n):

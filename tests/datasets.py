@@ -1,29 +1,36 @@
 """Seeded synthetic datasets of BASELINE.json configs 2-4 (test
-infrastructure): the same bytes whoever signs them, because RFC 8032 signing
-is deterministic -- libsodium here (tests/golden/make_digests.py, which commits
-SHA-256 digests of libsodium's expected accept bitmaps) and the GPU signer on
-the box (tests/test_gpu_digests.py, which checks libstl's bitmaps against
-those digests).
+infrastructure): the same bytes whoever builds them, because RFC 8032 signing
+is deterministic and every adversarial row is a fixed function of its own
+honest row -- libsodium here (tests/golden/make_digests.py, which commits
+SHA-256 digests of the inputs and of libsodium's expected accept bitmaps) and
+the GPU signer on the box (tests/test_gpu_digests.py, which checks libstl's
+bitmaps against those digests).
 
   config 2   1,048,576 valid signatures, seed 0x5EED0002 (= bench.py rank 0)
-  config 4   10,000,000 signatures, 2 % of rows replaced by golden adversarial
-             rows (every SURVEY Appendix-B class), chunks of 2,000,000 with
-             seed 0x5EED0004 + chunk offset
+  config 4   10,000,000 signatures, 2 % of the rows adversarial, split evenly
+             over SURVEY.md Appendix-B classes B1-B11 (B12 is a host-side
+             pre-reject), chunks of 2,000,000 with seed 0x5EED0004 + offset
   config 3   67,108,864 signatures, same construction, chunks of 4,194,304
              with seed 0x5EED0003 + chunk offset
 
 Row construction (per chunk): rng = default_rng(seed); seeds = 32 random
-bytes per row, msgs = 32 random bytes per row; (pk, sig) = sign(seeds, msgs);
-rows = rng.choice(n, int(n * frac), replace=False) are replaced by golden
-rows rng.integers(0, pool) of the non-valid classes -- the construction
-tools/report_configs.py used for the round-1 64M run.
+bytes per row, msgs = 32 random bytes per row; (pk, sig) = RFC 8032 keypair
+and signature; rows = rng.choice(n, n * frac, replace=False) get classes
+1 + (i mod 11) in that order and params = rng.integers(0, 2^32) each; row i
+of class c is then rebuilt from its own honest row by mutate() below (the
+device builds the same rows: stl_kernels.hip adversarial_row,
+stl_debug_sign_adversarial_device).  Every adversarial row is therefore
+distinct (its own key, message and signature).
 """
 import hashlib
 import os
+import sys
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+import ed25519_py as ed  # noqa: E402
 
 CONFIGS = {
     "config2": {"n": 1 << 20, "chunk": 1 << 20, "seed": 0x5EED0002, "frac": 0.0},
@@ -33,36 +40,161 @@ CONFIGS = {
 
 DIGESTS = os.path.join(ROOT, "tests", "golden", "bitmap_digests.json")
 
-
-def adversarial_pool():
-    g = np.load(os.path.join(ROOT, "tests", "golden", "ed25519_golden.npz"), allow_pickle=False)
-    names = [str(x) for x in g["class_names"]]
-    idx = np.nonzero(g["cls"] != names.index("valid"))[0]
-    return g["sig"][idx], g["msg"][idx], g["pk"][idx], g["cls"][idx], names
+CLASSES = ["valid", "B1_msg_bit", "B2_R_bit", "B3_S_bit", "B4_S_plus_L", "B5_S_top_bits", "B6_small_order_pk",
+           "B7_small_order_R", "B8_mixed_order_pk", "B9_noncanonical_pk", "B10_pk_not_on_curve",
+           "B11_noncanonical_R"]
+NCLASSES = len(CLASSES) - 1
 
 
-def chunk(seed, n, frac, sign, pool=None):
-    """One chunk: (sig, msg, pk, class counts).  sign(seeds, msgs) -> (pk, sig)
-    as uint8 numpy arrays."""
+def _small_order_encodings():
+    """The 14 encodings of points of order dividing 8 (both sign bits, y = p
+    and p + 1), sorted -- kSmallOrderEnc on the device."""
+    tors, _ = ed.torsion_points()
+    so = set()
+    for t in tors:
+        e = ed.encode(t)
+        so.add(e)
+        so.add(bytes(e[:31]) + bytes([e[31] ^ 0x80]))
+    so.update(ed.SMALL_ORDER_BLOCKLIST)
+    so.add(bytes(ed.SMALL_ORDER_BLOCKLIST[5][:31]) + bytes([0xFF]))
+    so.add(bytes(ed.SMALL_ORDER_BLOCKLIST[6][:31]) + bytes([0xFF]))
+    return sorted(so)
+
+
+SMALL_ORDER = _small_order_encodings()
+TORSION = [ed.encode(t) for t in ed.torsion_points()[0]]  # i * T8, kTorsionEnc
+NONCANON_R = [bytes.fromhex(h) for h in ("ee" + "ff" * 30 + "7f", "01" + "00" * 30 + "80", "ee" + "ff" * 30 + "ff")]
+S_TOP = (0xE0, 0x80, 0x40, 0x20)
+
+
+def _k_times_a(R, A, M, a):
+    return (ed.sha512_int(R, A, M) % ed.L) * a % ed.L
+
+
+def mutate_row(c, u, seed, A, sig, M, group):
+    """Class-c mutation with parameter u of one honest row (bytes) -> (A, sig,
+    M).  group: (scalarmult_base(S) -> 32 B, point_add(P, Q) -> 32 B)."""
+    R, S = bytearray(sig[:32]), bytearray(sig[32:])
+    A, M = bytearray(A), bytearray(M)
+    byte, bit = u % 32, 1 << ((u >> 5) & 7)
+    if c == 1:
+        M[byte] ^= bit
+    elif c == 2:
+        R[byte] ^= bit
+    elif c == 3:
+        s = int.from_bytes(S, "little")
+        b0 = u % 252
+        for i in range(252):
+            b = (b0 - i) % 252
+            if (s >> b) & 1:
+                s &= ~(1 << b)
+                break
+        S = bytearray(s.to_bytes(32, "little"))
+    elif c == 4:
+        S = bytearray((int.from_bytes(S, "little") + ed.L).to_bytes(32, "little"))
+    elif c == 5:
+        S[31] |= S_TOP[u % 4]
+    elif c == 6:
+        A = bytearray(SMALL_ORDER[u % 14])
+        R = bytearray(group[0](bytes(S)))
+    elif c in (7, 11):
+        if c == 11 and u % 2 == 0:
+            R[31] ^= 0x80
+        else:
+            R = bytearray(SMALL_ORDER[u % 14] if c == 7 else NONCANON_R[(u >> 1) % 3])
+            a, _ = ed.secret_scalar(seed)
+            S = bytearray(_k_times_a(bytes(R), bytes(A), bytes(M), a).to_bytes(32, "little"))
+    elif c == 8:
+        A = bytearray(group[1](bytes(A), TORSION[1 + u % 7]))
+        a, prefix = ed.secret_scalar(seed)
+        r = ed.sha512_int(prefix, bytes(M)) % ed.L  # R is the honest [r]B
+        S = bytearray(((r + ed.sha512_int(bytes(R), bytes(A), bytes(M)) % ed.L * a) % ed.L).to_bytes(32, "little"))
+    elif c == 9:
+        y = ed.P + 2 + u % 17
+        A = bytearray((y | (((u >> 8) & 1) << 255)).to_bytes(32, "little"))
+    elif c == 10:
+        v = int.from_bytes(A, "little")
+        sign, y = v >> 255, v & ((1 << 255) - 1)
+        for j in range(1, 65):
+            if y + j < ed.P and ed.recover_x(y + j, sign) is None:
+                A = bytearray(((y + j) | (sign << 255)).to_bytes(32, "little"))
+                break
+    return bytes(A), bytes(R) + bytes(S), bytes(M)
+
+
+def python_group():
+    """Group operations in pure Python (slow; for small cross-checks)."""
+    return (lambda S: ed.encode(ed.mul(int.from_bytes(S, "little"), ed.B)),
+            lambda P, Q: ed.encode(ed.add(ed.decode(P), ed.decode(Q))))
+
+
+def sodium_group(lib):
+    """Group operations through libsodium (oracle/_ref/libsodium_ref.so)."""
+    import ctypes
+
+    def smul(S):
+        out = ctypes.create_string_buffer(32)
+        assert lib.ref_scalarmult_base_noclamp(out, S) == 0
+        return out.raw
+
+    def padd(P, Q):
+        out = ctypes.create_string_buffer(32)
+        assert lib.ref_point_add(out, P, Q) == 0
+        return out.raw
+
+    return smul, padd
+
+
+def mutate(seeds, msgs, pk, sig, cls, param, group):
+    """Apply the class mutations in place to the rows with cls > 0 (uint8
+    arrays as built by chunk())."""
+    for i in np.nonzero(cls)[0]:
+        A, s, M = mutate_row(int(cls[i]), int(param[i]), bytes(seeds[i]), bytes(pk[i]), bytes(sig[i]),
+                             bytes(msgs[i]), group)
+        pk[i] = np.frombuffer(A, np.uint8)
+        sig[i] = np.frombuffer(s, np.uint8)
+        msgs[i] = np.frombuffer(M, np.uint8)
+
+
+def chunk_plan(seed, n, frac):
+    """(seeds, msgs, cls, param) of one chunk: the honest rows' inputs and the
+    adversarial class / parameter of every row (0 = honest)."""
     rng = np.random.default_rng(seed)
     seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
     msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-    pk, sig = sign(seeds, msgs)
-    pk, sig = np.array(pk, np.uint8, copy=True), np.array(sig, np.uint8, copy=True)
-    classes = {}
+    cls = np.zeros(n, np.uint8)
+    param = np.zeros(n, np.uint32)
     if frac > 0:
-        asig, amsg, apk, acls, names = pool if pool is not None else adversarial_pool()
         rows = rng.choice(n, int(n * frac), replace=False)
-        pick = rng.integers(0, asig.shape[0], rows.size)
-        sig[rows], msgs[rows], pk[rows] = asig[pick], amsg[pick], apk[pick]
-        classes = {names[c]: int((acls[pick] == c).sum()) for c in np.unique(acls[pick])}
-    return sig, msgs, pk, classes
+        cls[rows] = 1 + np.arange(rows.size) % NCLASSES
+        param[rows] = rng.integers(0, 1 << 32, rows.size, dtype=np.uint64).astype(np.uint32)
+    return seeds, msgs, cls, param
+
+
+def class_counts(cls):
+    return {CLASSES[c]: int((cls == c).sum()) for c in range(1, NCLASSES + 1) if (cls == c).any()}
+
+
+def chunk(seed, n, frac, make):
+    """One chunk: (sig, msg, pk, cls).  make(seeds, msgs, cls, param) ->
+    (pk, sig, msg) uint8 arrays: the honest rows with the mutations applied."""
+    seeds, msgs, cls, param = chunk_plan(seed, n, frac)
+    pk, sig, msg = make(seeds, msgs, cls, param)
+    return (np.ascontiguousarray(sig, np.uint8), np.ascontiguousarray(msg, np.uint8),
+            np.ascontiguousarray(pk, np.uint8), cls)
 
 
 def chunks(name):
     c = CONFIGS[name]
     for c0 in range(0, c["n"], c["chunk"]):
         yield c0, c["seed"] + (c0 if c["frac"] > 0 else 0), min(c["chunk"], c["n"] - c0), c["frac"]
+
+
+def row_keys(sig, msg, pk):
+    """A 16-byte key per row (first half of SHA-256 of its 128 bytes), for
+    counting distinct rows."""
+    rows = np.concatenate([sig, msg, pk], axis=1)
+    return np.array([hashlib.sha256(r.tobytes()).digest()[:16] for r in rows])
 
 
 class Digest:

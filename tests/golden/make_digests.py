@@ -15,6 +15,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
@@ -29,23 +31,32 @@ def main(names):
     if os.path.exists(datasets.DIGESTS):
         with open(datasets.DIGESTS) as f:
             out = json.load(f)
-    pool = datasets.adversarial_pool()
+    group = datasets.sodium_group(lib)
     for name in names:
         t0 = time.time()
         dg = datasets.Digest()
-        classes = {}
+        classes, keys = {}, []
 
-        def sign(seeds, msgs):
-            return oracle_bind.sodium_sign_batch(lib, seeds, msgs, threads)
+        def make(seeds, msgs, cls, param):
+            pk, sig = oracle_bind.sodium_sign_batch(lib, seeds, msgs, threads)
+            msgs = msgs.copy()
+            datasets.mutate(seeds, msgs, pk, sig, cls, param, group)
+            return pk, sig, msgs
 
         for c0, seed, n, frac in datasets.chunks(name):
-            sig, msg, pk, cls = datasets.chunk(seed, n, frac, sign, pool)
+            sig, msg, pk, cls = datasets.chunk(seed, n, frac, make)
             bits = oracle_bind.sodium_verify_batch(lib, sig, msg, pk, threads)
             dg.add(sig, msg, pk, bits)
-            for k, v in cls.items():
+            for k, v in datasets.class_counts(cls).items():
                 classes[k] = classes.get(k, 0) + v
+            adv = np.nonzero(cls)[0]
+            keys.append(datasets.row_keys(sig[adv], msg[adv], pk[adv]))
             print(f"{name}: rows {c0 + n} accepted {dg.accepted} ({time.time() - t0:.0f} s)", flush=True)
+        keys = np.concatenate(keys) if keys else np.zeros(0, "S16")
         out[name] = dict(dg.result(), **datasets.CONFIGS[name], adversarial_rows_by_class=classes,
+                         adversarial_rows_distinct=int(np.unique(keys).size),
+                         construction="each adversarial row mutated from its own honest row, classes B1-B11 "
+                                      "evenly (tests/datasets.py)",
                          expected_from=f"libsodium {lib.ref_sodium_version().decode()} "
                                        "crypto_sign_verify_detached && S < L")
         with open(datasets.DIGESTS, "w") as f:

@@ -41,6 +41,8 @@ class Oracle:
         V = ctypes.c_void_p
         lib.oracle_verify.restype = ctypes.c_int
         lib.oracle_verify.argtypes = [V, V, ctypes.c_size_t, V, ctypes.c_uint32]
+        lib.oracle_verify_raw.restype = ctypes.c_int
+        lib.oracle_verify_raw.argtypes = [V, V, ctypes.c_size_t, V, ctypes.c_uint32]
         lib.oracle_verify_batch.argtypes = [V, V, V, ctypes.c_size_t, V, ctypes.c_uint32, ctypes.c_int]
         lib.oracle_tx_verify_batch.argtypes = [V, V, V, V, V, ctypes.c_size_t, V, ctypes.c_uint32, ctypes.c_int]
         lib.oracle_sha512.argtypes = [V, ctypes.c_size_t, V]
@@ -57,6 +59,10 @@ class Oracle:
 
     def verify(self, sig, msg, pk, policy=0):
         return self.lib.oracle_verify(bytes(sig), bytes(msg), len(msg), bytes(pk), policy) == 0
+
+    def verify_raw(self, sig, msg, pk, policy=0):
+        """The bare crypto_sign_verify_detached predicate (no stellard S < L)."""
+        return self.lib.oracle_verify_raw(bytes(sig), bytes(msg), len(msg), bytes(pk), policy) == 0
 
     def verify_batch(self, sig, msg, pk, policy=0, threads=0):
         sig = np.ascontiguousarray(sig, np.uint8)

@@ -1,11 +1,15 @@
 """GPU parity at BASELINE.json's full sizes, pinned by committed data:
 libstl's accept bitmaps for the seeded datasets of configs 2 (1,048,576
-signatures), 4 (10,000,000, 2 % adversarial rows of every Appendix-B class)
-and 3 (67,108,864, same construction) against the SHA-256 digests of the
+signatures), 4 (10,000,000, 2 % adversarial rows split evenly over the
+Appendix-B classes B1-B11, each built from its own honest row) and 3
+(67,108,864, same construction) against the SHA-256 digests of the
 bitmaps libsodium 1.0.18 gave the same rows (tests/golden/bitmap_digests.json,
 made by tests/golden/make_digests.py in the build container).  The inputs are
-regenerated here with the GPU signer (RFC 8032 signing is deterministic; the
-input digest checks that) -- nothing from libsodium is needed on the box.
+regenerated here with the GPU signer and its adversarial-row builder
+(stl_debug_sign_adversarial_device: RFC 8032 signing is deterministic and the
+mutations are fixed functions of the honest row; the input digest checks that
+the device built the same bytes as libsodium + tests/datasets.py did) --
+nothing from libsodium is needed on the box.
 
 Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120
 """
@@ -41,16 +45,17 @@ def test_config_bitmap_digest(stl, torch_cuda, name):
     torch = torch_cuda
     with open(datasets.DIGESTS) as f:
         want = json.load(f)[name]
-    pool = datasets.adversarial_pool()
 
-    def sign(seeds, msgs):
-        pk, sig = stl.sign_batch_device(torch.from_numpy(seeds).cuda(), torch.from_numpy(msgs).cuda())
-        return pk.cpu().numpy(), sig.cpu().numpy()
+    def make(seeds, msgs, cls, param):
+        t = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (seeds, msgs, cls, param.view(np.int32))]
+        pk, sig, mo = stl.sign_adversarial_device(*t)
+        return pk.cpu().numpy(), sig.cpu().numpy(), mo.cpu().numpy()
 
     dg = datasets.Digest()
     t0, gpu_s = time.time(), 0.0
+    classes, keys = {}, []
     for c0, seed, n, frac in datasets.chunks(name):
-        sig, msg, pk, _ = datasets.chunk(seed, n, frac, sign, pool)
+        sig, msg, pk, cls = datasets.chunk(seed, n, frac, make)
         d = [torch.from_numpy(a).cuda() for a in (sig, msg, pk)]
         torch.cuda.synchronize()
         t1 = time.time()
@@ -58,9 +63,22 @@ def test_config_bitmap_digest(stl, torch_cuda, name):
         torch.cuda.synchronize()
         gpu_s += time.time() - t1
         dg.add(sig, msg, pk, stl.words_to_bool(words, n))
+        for k, v in datasets.class_counts(cls).items():
+            classes[k] = classes.get(k, 0) + v
+        adv = np.nonzero(cls)[0]
+        keys.append(datasets.row_keys(sig[adv], msg[adv], pk[adv]))
         print(f"{name}: rows {c0 + n} ({time.time() - t0:.1f} s)", flush=True)
     got = dg.result()
     assert got["rows"] == want["rows"]
+    assert classes == want["adversarial_rows_by_class"]
+    if classes:  # 2 % invalid, split evenly over the Appendix-B classes B1-B11
+        nadv = sum(classes.values())
+        assert len(classes) == datasets.NCLASSES
+        assert nadv == sum(int(n * frac) for _, _, n, frac in datasets.chunks(name))
+        even = nadv / datasets.NCLASSES
+        assert all(abs(v - even) <= 0.05 * even for v in classes.values()), classes
+        distinct = int(np.unique(np.concatenate(keys)).size)
+        assert distinct == want["adversarial_rows_distinct"] and distinct >= 0.95 * nadv, distinct
     assert got["inputs_sha256"] == want["inputs_sha256"], "GPU signer / dataset generation differs"
     assert got["accepted"] == want["accepted"], (got["accepted"], want["accepted"])
     assert got["bitmap_sha256"] == want["bitmap_sha256"]

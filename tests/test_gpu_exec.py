@@ -1,0 +1,146 @@
+"""GPU tests of libstl's execution settings (stl_debug_tuning): the fused
+phase-1 kernel, the main kernel's unit queue, and chunks over concurrent
+streams -- every setting must give the same accept bits as the two-kernel,
+grid-stride, one-stream path of round 2, and those bits are the oracle's.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def stl(torch_cuda):
+    from stellard_amd import verify
+    verify.init()
+    return verify
+
+
+SETTINGS = [  # (fused_prep, main_queue, streams, chunk_log2)
+    (0, 0, 1, 18), (1, 0, 1, 18), (0, 1, 1, 18), (1, 1, 1, 18),
+    (1, 1, 2, 18), (1, 1, 4, 18), (1, 1, 3, 17), (1, 1, 4, 16), (0, 0, 2, 19), (1, 1, 2, 20),
+]
+
+
+def _apply(stl, v):
+    old = []
+    for key, val in zip((stl.TUNE_FUSED_PREP, stl.TUNE_MAIN_QUEUE, stl.TUNE_STREAMS, stl.TUNE_CHUNK_LOG2), v):
+        old.append(stl.debug_tuning(key, val))
+    return tuple(old)
+
+
+@pytest.fixture(scope="module")
+def batch(stl, torch_cuda, golden):
+    """600,037 rows: GPU-signed valid signatures, 1 % with a flipped message
+    byte, and every 97th row a golden vector (all Appendix-B classes)."""
+    torch = torch_cuda
+    n = 600_037
+    rng = np.random.default_rng(77)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pk, sig = stl.sign_batch_device(torch.from_numpy(seeds).cuda(), torch.from_numpy(msgs).cuda())
+    sig, pk = sig.cpu().numpy(), pk.cpu().numpy()
+    flip = rng.choice(n, n // 100, replace=False)
+    msgs[flip, 3] ^= 0x10
+    rows = np.arange(0, n, 97)
+    pick = rng.integers(0, golden["sig"].shape[0], rows.size)
+    sig[rows], msgs[rows], pk[rows] = golden["sig"][pick], golden["msg"][pick], golden["pk"][pick]
+    exp_golden = golden["expected_sodium_1_0_18"][pick].astype(bool)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (sig, msgs, pk)]
+    return n, d, (sig, msgs, pk), rows, exp_golden, flip
+
+
+def _run(stl, torch, d, n, policy=0):
+    w = stl.verify_batch_device(*d, policy=policy)
+    torch.cuda.synchronize()
+    return stl.words_to_bool(w, n)
+
+
+def test_settings_same_bits(stl, torch_cuda, batch, oracle):
+    torch = torch_cuda
+    n, d, host, rows, exp_golden, flip = batch
+    old = _apply(stl, SETTINGS[0])
+    try:
+        ref = _run(stl, torch, d, n)
+        # the reference path's bits are the oracle's: golden rows exactly, the
+        # flipped rows rejected, and a 20,000-row sample re-checked
+        assert np.array_equal(ref[rows], exp_golden)
+        assert not ref[np.setdiff1d(flip, rows)].any()
+        sample = np.random.default_rng(5).choice(n, 20_000, replace=False)
+        assert np.array_equal(ref[sample], oracle.verify_batch(*(a[sample] for a in host)))
+        for v in SETTINGS[1:]:
+            _apply(stl, v)
+            got = _run(stl, torch, d, n)
+            assert np.array_equal(got, ref), (v, np.nonzero(got != ref)[0][:8])
+    finally:
+        _apply(stl, old)
+
+
+@pytest.mark.parametrize("flags", ["full_length", "dedup", "policy100"])
+def test_settings_same_bits_with_flags(stl, torch_cuda, batch, flags):
+    """The flag paths under concurrent streams: full-length lanes, key dedup
+    (each stream's workspace has its own key tables) and the 1.0.0 policy."""
+    torch = torch_cuda
+    n, d, host, rows, exp_golden, flip = batch
+    pol = {"full_length": stl.FULL_LENGTH, "dedup": stl.DEDUP_KEYS, "policy100": stl.POLICY_STELLARD_1_0_0}[flags]
+    old = _apply(stl, SETTINGS[0])
+    try:
+        ref = _run(stl, torch, d, n, pol)
+        for v in ((1, 1, 1, 18), (1, 1, 4, 16), (1, 1, 2, 18)):
+            _apply(stl, v)
+            assert np.array_equal(_run(stl, torch, d, n, pol), ref), (flags, v)
+    finally:
+        _apply(stl, old)
+    if flags != "policy100":
+        assert np.array_equal(ref, _run(stl, torch, d, n))
+
+
+def test_streams_with_caller_stream_and_phase_timing(stl, torch_cuda, batch):
+    """A call on a side stream forks the library's streams from it and joins
+    them back: work queued after the call on the same stream sees the whole
+    bitmap.  Under the phase clock the chunks run on one stream and every
+    chunk is timed."""
+    torch = torch_cuda
+    n, d, host, rows, exp_golden, flip = batch
+    old = _apply(stl, (1, 1, 4, 16))
+    try:
+        ref = _run(stl, torch, d, n)
+        s = torch.cuda.Stream()
+        w = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                w.zero_()
+                stl.verify_batch_device(*d, out_words=w, stream=s)
+            total = w.clone()  # on s: after the joined streams
+        torch.cuda.synchronize()
+        assert np.array_equal(stl.words_to_bool(total, n), ref)
+        stl.reset_stats()
+        stl.set_phase_timing(True)
+        try:
+            assert np.array_equal(_run(stl, torch, d, n), ref)
+            st = stl.get_stats()
+        finally:
+            stl.set_phase_timing(False)
+        assert st["phase_chunks"] == 1  # n < 2^20: one chunk, kernels one after another
+        assert st["phase_ns"]["main"] > 0
+    finally:
+        _apply(stl, old)
+
+
+def test_tuning_rejects_bad_values(stl):
+    from stellard_amd import _native as N
+    lib = N.load()
+    for key, bad in ((stl.TUNE_FUSED_PREP, 2), (stl.TUNE_MAIN_QUEUE, -2), (stl.TUNE_STREAMS, 0),
+                     (stl.TUNE_STREAMS, 5), (stl.TUNE_CHUNK_LOG2, 15), (stl.TUNE_CHUNK_LOG2, 21), (99, 1)):
+        assert lib.stl_debug_tuning(key, bad) == N.STL_EINVAL, (key, bad)
+    assert stl.execution_settings()["streams"] in (1, 2, 3, 4)

@@ -144,10 +144,21 @@ def test_mixed_fallback_lanes_in_one_wave(stl, torch_cuda, oracle):
 
 
 # ------------------------------------------------------- multi-shard / RCCL
-@pytest.mark.parametrize("mode", ["shards3", "rccl1"])
+@pytest.mark.parametrize("mode", ["shards3", "rccl1", "rccl1_bytes"])
 def test_host_paths_multi_shard_and_rccl(stl, oracle, golden, mode):
+    """rccl1_bytes: the byte-balanced shard path on one device (test hook
+    STL_TUNE_BYTE_SHARDS) -- the grouped gather's placement and rank 0's own
+    device copy run for the preimage and blob batches."""
     from stellard_amd import _native as N
     cfg = dict(shards_per_device=3) if mode == "shards3" else dict(flags=N.STL_CFG_RCCL_GATHER)
+    prev = stl.debug_tuning(stl.TUNE_BYTE_SHARDS, 1 if mode == "rccl1_bytes" else 0)
+    try:
+        _host_paths(stl, oracle, golden, mode, cfg)
+    finally:
+        stl.debug_tuning(stl.TUNE_BYTE_SHARDS, prev)
+
+
+def _host_paths(stl, oracle, golden, mode, cfg):
     from tests import txblob
     blobs = txblob.valid_corpus(oracle, 400, 31)
     rng = np.random.default_rng(32)
@@ -323,8 +334,8 @@ def test_phase_timing(stl, golden, torch_cuda):
         st = stl.get_stats()
         assert st["phase_chunks"] == 2, st
         ph = st["phase_ns"]
-        assert all(ph[k] > 0 for k in ("scalar", "point", "main")), ph
-        assert ph["main"] > ph["scalar"], ph
+        assert all(ph[k] > 0 for k in ("phase1", "main")), ph  # "point" is 0 with the fused phase-1 kernel
+        assert ph["main"] > ph["phase1"], ph
     finally:
         stl.set_phase_timing(False)
     stl.verify_batch(sig, msg, pk)
@@ -471,3 +482,56 @@ def test_proposals_vs_oracle(stl, oracle):
     got = stl.tx_verify_batch(pres, sig, pk)
     assert np.array_equal(got, exp)
     assert 300 < exp.sum() < 400
+
+
+# --------------------------------------------- single call: caller fallback
+def test_fallback_verify_answers_device_failures(stl, oracle, golden):
+    """stl_config.fallback_verify (ABI 3): with the caller's own check
+    registered (stellard: libsodium's crypto_sign_verify_detached; the oracle's
+    raw libsodium-1.0.18 predicate here), stl_ed25519_verify_detached returns
+    only 0 or -1 -- a failed device call is answered by the fallback composed
+    with S < L, never reported as a reject (RippleAddress.cpp:196-199).
+    Without a fallback the same failure is an error code below -1."""
+    import ctypes
+
+    from stellard_amd import _native as N
+    sig, msg, pk, exp = _golden_rows(golden, 40, seed=17)
+    calls = []
+
+    def fb(s, m, mlen, p):
+        calls.append(mlen)
+        return 0 if oracle.verify_raw(ctypes.string_at(s, 64), ctypes.string_at(m, mlen),
+                                      ctypes.string_at(p, 32), policy=0) else -1
+
+    fn = stl.VERIFY_FN(fb)
+    lib = N.load()
+    with reinit(stl, fallback_verify=fn):
+        for i in range(40):
+            for k in range(0, 10):
+                stl.debug_fault_after(k)
+                rc = lib.stl_ed25519_verify_detached(sig[i].tobytes(), msg[i].tobytes(), 32, pk[i].tobytes())
+                stl.debug_fault_after(-1)
+                assert rc in (0, -1), (i, k, rc)
+                assert (rc == 0) == bool(exp[i]), (i, k, rc)
+        assert len(calls) >= 40 and set(calls) == {32}
+    stl.debug_fault_after(0)
+    rc = lib.stl_ed25519_verify_detached(sig[0].tobytes(), msg[0].tobytes(), 32, pk[0].tobytes())
+    stl.debug_fault_after(-1)
+    assert rc < -1
+
+
+def test_comm_info(stl):
+    """stl_comm_info: what RCCL reports for the communicator libstl gathers
+    over (ncclCommCount / ncclCommUserRank) -- the bench asserts it equals
+    WORLD_SIZE on every rank before timing."""
+    from stellard_amd import _native as N
+    with pytest.raises(N.StlError) as e:  # the default init builds no in-process communicator
+        stl.comm_info()
+    assert e.value.rc == N.STL_ERCCL
+    stl.comm_init_rank(1, 0, stl.comm_unique_id())
+    try:
+        assert stl.comm_info() == (1, 0)
+    finally:
+        stl.comm_destroy()
+    with reinit(stl, flags=N.STL_CFG_RCCL_GATHER):
+        assert stl.comm_info() == (1, 0)

@@ -49,6 +49,7 @@ def test_bench_launcher_dry_run(gpus):
     assert line["steps"] == 2 and line["warmup"] == 1 and line["scaling"] == "weak"
     assert line["config"]["gathered_all_ones"] is True
     assert line["config"]["rank0_shard"] == [0, 4160]
+    assert line["config"]["rccl_nranks"] == gpus  # the GPU run reads it from libstl's stl_comm_info
     assert line["metric"].startswith("DRY RUN")
 
 
@@ -220,7 +221,51 @@ def test_stats_without_gpu():
     bad = V.Stats()
     bad.struct_size = 8
     assert N.load().stl_get_stats(ctypes.byref(bad)) == N.STL_EINVAL
-    assert st["phase_chunks"] == 0 and set(st["phase_ns"]) == {"scalar", "point", "main", "fallback"}
+    assert st["phase_chunks"] == 0 and set(st["phase_ns"]) == {"phase1", "point", "main", "fallback"}
     # the phase-timing switch returns the previous setting
     assert V.set_phase_timing(True) is False
     assert V.set_phase_timing(False) is True
+
+
+def test_fallback_verify_without_gpu(oracle, golden):
+    """stl_config.fallback_verify on a host without a gfx950 device: stl_init
+    fails (ENODEV) but registers the caller's check, and the single call then
+    answers every signature with it (composed with S < L) -- 0 / -1 only, the
+    exact golden bits.  Registering NULL again restores the error code."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    from stellard_amd import _native as N
+    from stellard_amd import verify as V
+
+    def fb(s, m, mlen, p):
+        return 0 if oracle.verify_raw(ctypes.string_at(s, 64), ctypes.string_at(m, mlen), ctypes.string_at(p, 32),
+                                      policy=0) else -1
+
+    fn = V.VERIFY_FN(fb)
+    lib = N.load()
+    try:
+        with pytest.raises(N.StlError) as e:
+            V.init(fallback_verify=fn)
+        assert e.value.rc == N.STL_ENODEV
+        exp = golden["expected_sodium_1_0_18"].astype(bool)
+        idx = np.random.default_rng(4).choice(exp.shape[0], 300, replace=False)
+        for i in idx:
+            rc = lib.stl_ed25519_verify_detached(golden["sig"][i].tobytes(), golden["msg"][i].tobytes(), 32,
+                                                 golden["pk"][i].tobytes())
+            assert rc in (0, -1) and (rc == 0) == bool(exp[i]), (i, rc)
+    finally:
+        with pytest.raises(N.StlError):
+            V.init()  # registers NULL
+    assert lib.stl_ed25519_verify_detached(golden["sig"][0].tobytes(), golden["msg"][0].tobytes(), 32,
+                                           golden["pk"][0].tobytes()) == N.STL_ENODEV
+
+
+def test_comm_info_without_communicator():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    from stellard_amd import _native as N
+    nr, r = ctypes.c_int(-5), ctypes.c_int(-5)
+    assert N.load().stl_comm_info(ctypes.byref(nr), ctypes.byref(r)) == N.STL_ERCCL
+    assert N.load().stl_comm_info(None, None) == N.STL_EINVAL

@@ -57,6 +57,24 @@ def test_rippleaddress_kat(oracle):
     nc = sig[:32] + S.to_bytes(32, "little")
     assert not oracle.verify(nc, msg, pk, policy=0)
     assert not oracle.verify(nc, msg, pk, policy=1)
+    # the bare libsodium call on the S+L signature (RippleAddress.cpp:841-844):
+    # the reference expects it to VERIFY -- true of the 1.0.0 predicate it pins
+    # (Dockerfile:9-10), false of 1.0.18, which rejects S >= L itself
+    assert oracle.verify_raw(nc, msg, pk, policy=1)
+    assert not oracle.verify_raw(nc, msg, pk, policy=0)
+    assert oracle.verify_raw(sig, msg, pk, policy=0) and oracle.verify_raw(sig, msg, pk, policy=1)
+    ref = oracle_bind.load_sodium_ref()
+    if ref is not None:  # the container's libsodium 1.0.18 itself
+        assert ref.ref_crypto_sign_verify_detached(nc, msg, 32, pk) == -1
+        assert ref.ref_crypto_sign_verify_detached(sig, msg, 32, pk) == 0
+    # the device verify code compiled for the host, in raw mode (core policy bit 1)
+    emu = oracle_bind.load_hostemu()
+    rows = [np.frombuffer(x, np.uint8).reshape(1, -1) for x in (nc, msg, pk)]
+    for pol, want in ((1 | 2, 1), (1, 0), (0 | 2, 0), (0, 0)):
+        bm = np.zeros(1, np.uint8)
+        emu.hostemu_verify_batch(*[oracle_bind._buf(np.ascontiguousarray(r)) for r in rows], 1,
+                                 oracle_bind._buf(bm), pol)
+        assert int(bm[0] & 1) == want, (pol, bm)
 
 
 def test_oracle_sha512(oracle):
