@@ -20,7 +20,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 PRODUCT_SRCS = ["stl_kernels.hip", "stl_api.cpp", "stl_batcher.cpp"]
 PRODUCT_DEPS = PRODUCT_SRCS + ["stl_kernels.h", "stl_verify_core.h", "stl_fe25519.h", "stl_ge25519.h",
-                               "stl_sc25519.h", "stl_sha512.h", "stl_base_table.h", "stl_lattice.h", "stl_txblob.h",
+                               "stl_sc25519.h", "stl_sha512.h", "stl_base_table.h", "stl_lattice.h", "stl_txblob.h", "stl_sign.h",
                                os.path.join("..", "..", "include", "stl.h")]
 
 

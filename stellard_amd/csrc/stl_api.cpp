@@ -245,7 +245,7 @@ void phase_mark(void* ctx, hipStream_t s, int i) {
 // and streams.  Every setting gives the same accept bits (tests run them all).
 std::atomic<int> g_tune_fused{1};     // phase 1 as one kernel
 std::atomic<int> g_tune_queue{1};     // main kernel pulls units from a counter
-std::atomic<int> g_tune_streams{1};   // concurrent streams per device-resident call
+std::atomic<int> g_tune_streams{2};   // concurrent streams per device-resident call (A/B: DESIGN.md section 8)
 std::atomic<int> g_tune_sub_log2{18}; // signatures per stream chunk
 std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
 

@@ -22,6 +22,7 @@
 // resident lanes.
 #include "stl_base_table.h"
 #include "stl_kernels.h"
+#include "stl_sign.h"
 #include "stl_txblob.h"
 #include "stl_verify_core.h"
 
@@ -1066,191 +1067,9 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
   }
 }
 
-// SHA-512 of a short word-aligned input (nwords even, nwords*4 <= 108 bytes).
-__device__ __forceinline__ void sha512_short(uint32_t out[16], const uint32_t* in, int nwords) {
-  uint64_t st[8], w[16];
-  sha512_init(st);
-#pragma unroll
-  for (int j = 0; j < 16; ++j) w[j] = 0;
-  for (int j = 0; j < nwords / 2; ++j) w[j] = be64_from_le32(in[2 * j], in[2 * j + 1]);
-  w[nwords / 2] = 0x8000000000000000ULL;
-  w[15] = (uint64_t)nwords * 32;
-  sha512_compress(st, w);
-  sha512_digest_le32(out, st);
-}
-
-// ---- adversarial rows of the full-size parity datasets (test data only) ----
-// SURVEY.md Appendix B classes, each built from a row's own honest signature
-// (tests/datasets.py holds the same construction on the host, over libsodium;
-// the input digests of the committed datasets pin the two against each other).
-// u is the row's 32-bit parameter.
-//   1 B1   msg byte u%32 ^= 1 << ((u>>5)&7)
-//   2 B2   R   byte u%32 ^= 1 << ((u>>5)&7)
-//   3 B3   clear the first set bit of S at or below bit u%252, scanning down
-//          (wrapping from 0 to 251): S stays < L
-//   4 B4   S += L
-//   5 B5   sig[63] |= {0xE0, 0x80, 0x40, 0x20}[u%4] (S >= 2^253)
-//   6 B6   pk = kSmallOrderEnc[u%14], R = encode([S]B)
-//   7 B7   R = kSmallOrderEnc[u%14], S = k*a mod L, k = H(R||A||M) mod L
-//   8 B8   pk = A' = A + kTorsionEnc[1 + u%7], S = r + k*a, k = H(R||A'||M)
-//   9 B9   pk = p + 2 + u%17 (non-canonical y), sign bit (u>>8)&1
-//  10 B10  pk = y + j | sign, the first j in 1..64 with y + j < p not on the curve
-//  11 B11  u even: R's sign bit flipped; u odd: R = kNonCanonR[(u>>1)%3], S = k*a
-__constant__ uint32_t kSmallOrderEnc[14][8] = {
-    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
-    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
-    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
-    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x85fc536du},
-    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
-    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0xfa03ac92u},
-    {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
-    {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu},
-    {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
-    {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu},
-    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
-    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu}};
-// i * T8, i = 0..7 (T8 = the order-8 point encoded 26e8...05)
-__constant__ uint32_t kTorsionEnc[8][8] = {
-    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
-    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
-    {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
-    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0xfa03ac92u},
-    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
-    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x85fc536du}};
-// non-canonical encodings of the identity: y = p + 1; y = 1 with the sign bit; both
-__constant__ uint32_t kNonCanonR[3][8] = {
-    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
-    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x80000000u},
-    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu}};
-
-__device__ __forceinline__ void copy8(uint32_t d[8], const uint32_t s[8]) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) d[i] = s[i];
-}
-
-// x (8 words) += y (8 words), mod 2^256
-__device__ __forceinline__ void add256(uint32_t x[8], const uint32_t y[8]) {
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)x[i] + y[i];
-    x[i] = (uint32_t)c;
-    c >>= 32;
-  }
-}
-
-// Mutates one honest row (A, R, S, M; a the clamped secret scalar, r the
-// nonce) into class `c` with parameter u (table above).
-__device__ void adversarial_row(uint32_t c, uint32_t u, uint32_t A[8], uint32_t R[8], uint32_t S[8], uint32_t M[8],
-                                const uint32_t a[8], const uint32_t r[8], const TableView& tv, const uint32_t* sB) {
-  const uint32_t byte = u % 32u, bit = 1u << ((u >> 5) & 7u);
-  uint32_t zero[8], k[8], h[16];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) zero[i] = 0;
-  switch (c) {
-    case 1: M[byte >> 2] ^= bit << (8 * (byte & 3u)); break;
-    case 2: R[byte >> 2] ^= bit << (8 * (byte & 3u)); break;
-    case 3: {
-      const uint32_t b0 = u % 252u;
-      for (uint32_t s = 0; s < 252u; ++s) {
-        const uint32_t b = (b0 + 252u - s) % 252u;
-        if ((S[b >> 5] >> (b & 31u)) & 1u) {
-          S[b >> 5] &= ~(1u << (b & 31u));
-          break;
-        }
-      }
-      break;
-    }
-    case 4: {
-      uint32_t Lw[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) Lw[i] = sc_L(i);
-      add256(S, Lw);
-      break;
-    }
-    case 5: {
-      const uint32_t pat[4] = {0xE0u, 0x80u, 0x40u, 0x20u};
-      S[7] |= pat[u % 4u] << 24;
-      break;
-    }
-    case 6: {
-      copy8(A, kSmallOrderEnc[u % 14u]);
-      ge_p3 id;
-      ge_p3_0(id);
-      ge_p2 P;
-      double_scalarmult(P, id, zero, S, tv, sB);  // [S]B
-      ge_tobytes(R, P);
-      break;
-    }
-    case 7:
-    case 11: {
-      if (c == 11 && (u & 1u) == 0) {
-        R[7] ^= 0x80000000u;
-        break;
-      }
-      copy8(R, c == 7 ? kSmallOrderEnc[u % 14u] : kNonCanonR[(u >> 1) % 3u]);
-      sha512_hram32(h, R, A, M);
-      sc_reduce64(k, h);
-      sc_muladd(S, k, a, zero);  // [S]B - [k]A = O
-      break;
-    }
-    case 8: {
-      ge_p3 nA, nT;
-      uint32_t T[8];
-      copy8(T, kTorsionEnc[1u + u % 7u]);
-      ge_frombytes_negate_vartime(nA, A);
-      ge_frombytes_negate_vartime(nT, T);
-      ge_cached cT;
-      ge_p3_to_cached(cT, nT);
-      ge_p1p1 t;
-      ge_add_cached(t, nA, cT);  // -(A + T)
-      ge_p2 s;
-      ge_p1p1_to_p2(s, t);
-      fe_neg(s.X, s.X);
-      ge_tobytes(A, s);
-      sha512_hram32(h, R, A, M);
-      sc_reduce64(k, h);
-      sc_muladd(S, k, a, r);
-      break;
-    }
-    case 9: {
-      const uint32_t j = 2u + u % 17u;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) A[i] = i == 0 ? 0xffffffedu + j : (i == 7 ? 0x7fffffffu : 0xffffffffu);
-      A[7] |= ((u >> 8) & 1u) << 31;
-      break;
-    }
-    case 10: {
-      const uint32_t sign = A[7] & 0x80000000u;
-      uint32_t y[8];
-      copy8(y, A);
-      y[7] &= 0x7fffffffu;
-      for (uint32_t j = 1; j <= 64u; ++j) {
-        uint32_t one[8] = {1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        add256(y, one);
-        if (!point_is_canonical(y) || (y[7] >> 31) != 0) continue;
-        uint32_t cand[8];
-        copy8(cand, y);
-        cand[7] |= sign;
-        ge_p3 tmp;
-        if (!ge_frombytes_negate_vartime(tmp, cand)) {
-          copy8(A, cand);
-          break;
-        }
-      }
-      break;
-    }
-    default: break;
-  }
-}
-
-// RFC 8032 keypair + signature per row; with `cls` (test data only) rows
-// whose class is not 0 are then mutated by adversarial_row and msg_out gets
-// the (possibly mutated) message.
+// RFC 8032 keypair + signature per row (stl_sign.h); with `cls` (test data
+// only) rows whose class is not 0 are then mutated by adversarial_row and
+// msg_out gets the (possibly mutated) message.
 template <bool ADV>
 __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restrict__ seed,
                                                       const uint8_t* __restrict__ msg, uint32_t n,
@@ -1266,42 +1085,10 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
     const uint32_t i = base + threadIdx.x;
     const bool live = i < n;
     const size_t j = live ? i : (n - 1);
-    uint32_t sd[8], M[8], h[16];
+    uint32_t sd[8], M[8], A[8], R[8], S[8], a[8], r[8];
     ld8(sd, seed + 32 * j);
     ld8(M, msg + 32 * j);
-    sha512_short(h, sd, 8);
-    uint32_t a[8], pre[16];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a[q] = h[q];
-    a[0] &= 0xfffffff8u;            // clamp: h[0] &= 248
-    a[7] = (a[7] & 0x7fffffffu) | 0x40000000u;  // h[31] &= 127; h[31] |= 64
-    uint32_t x[16], a_red[8], zero[8];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) x[q] = q < 8 ? a[q] : 0u;
-    sc_reduce64(a_red, x);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) zero[q] = 0;
-    ge_p3 id;
-    ge_p3_0(id);
-    ge_p2 P;
-    uint32_t A[8];
-    double_scalarmult(P, id, zero, a_red, tv, sB);  // A = [a]B
-    ge_tobytes(A, P);
-    // r = SHA-512(h[32..63] || M) mod L
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      pre[q] = h[8 + q];
-      pre[8 + q] = M[q];
-    }
-    uint32_t rh[16], r[8], R[8];
-    sha512_short(rh, pre, 16);
-    sc_reduce64(r, rh);
-    double_scalarmult(P, id, zero, r, tv, sB);      // R = [r]B
-    ge_tobytes(R, P);
-    uint32_t kh[16], k[8], S[8];
-    sha512_hram32(kh, R, A, M);
-    sc_reduce64(k, kh);
-    sc_muladd(S, k, a, r);                                   // S = r + k a mod L
+    sign_row(A, R, S, a, r, sd, M, tv, sB);
     if (ADV) {
       const uint32_t c = cls[j];
       if (c != 0) adversarial_row(c, param[j], A, R, S, M, a, r, tv, sB);

@@ -24,6 +24,7 @@ static void hostemu_check_subk(const stl::fe& a, const stl::fe& b, int k);
 #include "../../stellard_amd/csrc/stl_base_table.h"
 #include "../../stellard_amd/csrc/stl_txblob.h"
 #include "../../stellard_amd/csrc/stl_verify_core.h"
+#include "../../stellard_amd/csrc/stl_sign.h"
 
 static double alpha(const stl::fe& a) {
   uint32_t m = 0;
@@ -374,5 +375,30 @@ void hostemu_fe_invert_bytes(const uint8_t a[32], uint8_t out[32]) {
   stl::fe_invert(fo, fa);
   stl::fe_tobytes(wo, fo);
   std::memcpy(out, wo, 32);
+}
+
+// stl_sign.h on the host: the honest rows and the adversarial rows the GPU's
+// sign kernel builds (stl_debug_sign_adversarial_device), on 8 threads.
+void hostemu_sign_adversarial(const uint8_t* seed, const uint8_t* msg, const uint8_t* cls, const uint32_t* param,
+                              size_t n, uint8_t* pk, uint8_t* sig, uint8_t* msg_out) {
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < 8; ++t)
+    th.emplace_back([=] {
+      std::vector<uint4> table(81);
+      const stl::TableView tv = stl::TableView::contiguous(table.data());
+      const uint32_t* btab = &stl::kBaseNielsHost[0][0][0];
+      for (size_t i = t; i < n; i += 8) {
+        uint32_t sd[8], M[8], A[8], R[8], S[8], a[8], r[8];
+        load8(sd, seed + 32 * i);
+        load8(M, msg + 32 * i);
+        stl::sign_row(A, R, S, a, r, sd, M, tv, btab);
+        if (cls && cls[i]) stl::adversarial_row(cls[i], param[i], A, R, S, M, a, r, tv, btab);
+        std::memcpy(pk + 32 * i, A, 32);
+        std::memcpy(sig + 64 * i, R, 32);
+        std::memcpy(sig + 64 * i + 32, S, 32);
+        std::memcpy(msg_out + 32 * i, M, 32);
+      }
+    });
+  for (auto& x : th) x.join();
 }
 }

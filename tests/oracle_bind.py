@@ -235,6 +235,19 @@ def hostemu_signed_blob(lib, kind, blob):
     return st.value, msg.raw, idb.raw
 
 
+def hostemu_sign_adversarial(lib, seeds, msgs, cls, param):
+    """stl_sign.h compiled for the host: (pk, sig, msg) of the rows the GPU's
+    sign kernel builds."""
+    n = seeds.shape[0]
+    seeds, msgs = np.ascontiguousarray(seeds, np.uint8), np.ascontiguousarray(msgs, np.uint8)
+    cls, param = np.ascontiguousarray(cls, np.uint8), np.ascontiguousarray(param, np.uint32)
+    pk = np.empty((n, 32), np.uint8)
+    sig = np.empty((n, 64), np.uint8)
+    mo = np.empty((n, 32), np.uint8)
+    lib.hostemu_sign_adversarial(_buf(seeds), _buf(msgs), _buf(cls), _buf(param), n, _buf(pk), _buf(sig), _buf(mo))
+    return pk, sig, mo
+
+
 def hostemu_tx_blob(lib, blob):
     """Device pass compiled for the host: (status, msg, txid, layout)."""
     st = ctypes.c_uint32(0)
@@ -271,6 +284,7 @@ def load_hostemu():
     lib.hostemu_signed_blob.argtypes = [ctypes.c_uint32, V, ctypes.c_uint32, V, V, V]
     lib.hostemu_blob_words.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, V]
     lib.hostemu_wide_row.argtypes = [ctypes.c_int, ctypes.c_uint32, V]
+    lib.hostemu_sign_adversarial.argtypes = [V, V, V, V, ctypes.c_size_t, V, V, V]
     lib.hostemu_window_blocks.restype = ctypes.c_uint32
     lib.hostemu_window_blocks.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
     return lib

@@ -1,0 +1,102 @@
+"""The full-size datasets' construction (tests/datasets.py), on the CPU:
+
+* the GPU's row builder (stellard_amd/csrc/stl_sign.h, compiled for the host
+  by tests/native/hostemu.cpp) equals the host construction over libsodium
+  byte for byte, honest rows and every Appendix-B class B1-B11;
+* libsodium's verdicts on those rows equal the independent Python
+  restatement's (tests/golden/ed25519_py.py) for both policies' classes;
+* configs 3 and 4 plan an even class split, and every adversarial row is its
+  own (distinct) row.
+"""
+import numpy as np
+import pytest
+
+from tests import datasets, oracle_bind
+
+
+@pytest.fixture(scope="module")
+def sodium():
+    lib = oracle_bind.load_sodium_ref()
+    if lib is None:
+        pytest.skip("libsodium not present")
+    return lib
+
+
+@pytest.fixture(scope="module")
+def rows(sodium):
+    n = 6000
+    seeds, msgs, cls, param = datasets.chunk_plan(0x5EED0098, n, 0.6)
+    pk, sig = oracle_bind.sodium_sign_batch(sodium, seeds, msgs, 8)
+    m = msgs.copy()
+    datasets.mutate(seeds, m, pk, sig, cls, param, datasets.sodium_group(sodium))
+    return seeds, msgs, cls, param, pk, sig, m
+
+
+def test_device_code_builds_the_same_rows(rows):
+    seeds, msgs, cls, param, pk, sig, m = rows
+    emu = oracle_bind.load_hostemu()
+    pk_e, sig_e, m_e = oracle_bind.hostemu_sign_adversarial(emu, seeds, msgs, cls, param)
+    for c in range(datasets.NCLASSES + 1):
+        sel = cls == c
+        assert sel.any()
+        same = (pk_e[sel] == pk[sel]).all(1) & (sig_e[sel] == sig[sel]).all(1) & (m_e[sel] == m[sel]).all(1)
+        assert same.all(), (datasets.CLASSES[c], int((~same).sum()))
+
+
+def test_python_group_ops_agree(rows):
+    """The libsodium group operations behind B6 / B8 against the pure-Python
+    ones on a sample."""
+    seeds, msgs, cls, param, pk, sig, m = rows
+    idx = np.nonzero((cls == 6) | (cls == 8))[0][:60]
+    pk_h, sig_h = pk.copy(), sig.copy()
+    sub = np.zeros(cls.shape, np.uint8)
+    sub[idx] = cls[idx]
+    # rebuild the sampled rows from honest ones with pure-Python group ops
+    from tests import oracle_bind as ob
+    lib = ob.load_sodium_ref()
+    pk2, sig2 = ob.sodium_sign_batch(lib, seeds[idx], msgs[idx], 4)
+    m2 = msgs[idx].copy()
+    datasets.mutate(seeds[idx], m2, pk2, sig2, cls[idx], param[idx], datasets.python_group())
+    assert np.array_equal(pk2, pk_h[idx]) and np.array_equal(sig2, sig_h[idx]) and np.array_equal(m2, m[idx])
+
+
+def test_verdicts_per_class(rows, sodium):
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import ed25519_py as ed
+    seeds, msgs, cls, param, pk, sig, m = rows
+    bits = oracle_bind.sodium_verify_batch(sodium, sig, m, pk, 8)
+    assert bits[cls == 0].all()
+    for c in (1, 2, 3, 4, 5, 6, 7, 9, 10, 11):
+        assert not bits[cls == c].any(), datasets.CLASSES[c]
+    b8 = bits[cls == 8]
+    assert 0 < b8.sum() < b8.size  # accepted iff 8 | k (order-8 T), 4 | k, 2 | k
+    sample = np.nonzero(cls)[0][::9]
+    for pol in ("1.0.18", "1.0.0"):
+        py = np.array([ed.verify(sig[i].tobytes(), m[i].tobytes(), pk[i].tobytes(), pol) for i in sample])
+        if pol == "1.0.18":
+            assert np.array_equal(py, bits[sample])
+        else:  # 1.0.0: small-order keys / R pass when the equation holds
+            assert py[cls[sample] == 6].any() or py[cls[sample] == 7].any()
+
+
+@pytest.mark.parametrize("name", ["config4", "config3"])
+def test_plan_even_and_distinct(name):
+    total = {}
+    first = None
+    for c0, seed, n, frac in datasets.chunks(name):
+        _, _, cls, param = datasets.chunk_plan(seed, n, frac)
+        for k, v in datasets.class_counts(cls).items():
+            total[k] = total.get(k, 0) + v
+        if first is None:
+            first = (cls, param)
+        if name == "config3" and c0 >= 3 * (1 << 22):
+            break  # a quarter of the 64M plan is enough here
+    nadv = sum(total.values())
+    assert len(total) == datasets.NCLASSES
+    even = nadv / datasets.NCLASSES
+    assert all(abs(v - even) <= 0.05 * even for v in total.values()), total
+    cls, param = first
+    adv = np.nonzero(cls)[0]
+    assert np.unique(param[adv]).size > 0.99 * adv.size  # parameters drawn per row

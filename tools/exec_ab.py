@@ -20,8 +20,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from stellard_amd import verify as V  # noqa: E402
 
-DEFAULT = ["base=0,0,1,18", "fused=1,0,1,18", "queue=0,1,1,18", "fq=1,1,1,18", "fq_s2_18=1,1,2,18",
-           "fq_s4_18=1,1,4,18", "fq_s2_17=1,1,2,17", "fq_s4_17=1,1,4,17", "fq_s3_18=1,1,3,18", "q_s4_18=0,1,4,18"]
+DEFAULT = ["base=0,0,1,18", "fq=1,1,1,18", "q_s2_18=0,1,2,18", "fq_s2_18=1,1,2,18", "fq_s2_19=1,1,2,19",
+           "fq_s3_18=1,1,3,18", "fq_s4_18=1,1,4,18", "fq_s2_17=1,1,2,17", "fq_s3_17=1,1,3,17", "fq_s4_16=1,1,4,16"]
 
 
 def main():
