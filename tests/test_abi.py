@@ -31,6 +31,21 @@ def test_library_exports_every_declared_symbol():
     assert set(declared_symbols()) == bound
 
 
+def test_python_constants_match_header():
+    """Every numeric STL_* macro of include/stl.h has the same value in
+    stellard_amd/_native.py (the ctypes mirror the tests and bench use)."""
+    from stellard_amd import _native
+    with open(os.path.join(ROOT, "include", "stl.h")) as f:
+        text = f.read()
+    macros = dict(re.findall(r"#define\s+(STL_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+))u?\)?", text))
+    assert len(macros) > 20
+    missing = sorted(m for m in macros if m != "STL_ABI_VERSION" and not hasattr(_native, m))
+    assert not missing, missing
+    for m, v in macros.items():
+        if hasattr(_native, m):
+            assert getattr(_native, m) == int(v, 0), m
+
+
 def test_library_is_gfx950_code_object():
     from stellard_amd import _native
     with open(_native.LIB_PATH, "rb") as f:
