@@ -603,11 +603,21 @@ def gpu_run(args, world, rank, local):
         main_ms = phase_ms["main"]
         achieved = W_VERIFY * n / (main_ms * 1e-3) / 1e12
         achieved_launch = W_VERIFY * per_launch / 1e12
-        traffic = None
+        traffic, traffic_build = None, None
+        from stellard_amd.build import source_digest
+        digest = source_digest()
+
+        def provenance(doc, path):
+            b = dict(doc.get("build") or {})
+            b["file"] = os.path.relpath(path, ROOT)
+            b["matches_current_sources"] = b.get("sources_sha256") == digest
+            return b
         tp = os.path.join(ROOT, "profiles", "traffic_latest.json")
         if os.path.exists(tp):
             with open(tp) as f:
-                traffic = (json.load(f).get("main_kernel") or {}).get("hbm_bytes_per_launch")
+                td = json.load(f)
+            traffic = (td.get("main_kernel") or {}).get("hbm_bytes_per_launch")
+            traffic_build = provenance(td, tp)
         valu_busy = None
         vp = os.path.join(ROOT, "profiles", "valu_latest.json")
         if os.path.exists(vp):
@@ -615,7 +625,8 @@ def gpu_run(args, world, rank, local):
                 vd = json.load(f)
             valu_busy = {"launch_pct": vd.get("launch_valu_busy_pct"),
                          "per_kernel_pct": {k: v.get("VALUBusy") for k, v in vd.get("kernels", {}).items()},
-                         "source": vd.get("source", "rocprofv3 --pmc VALUBusy, profiles/valu_latest.json")}
+                         "source": vd.get("source", "rocprofv3 --pmc VALUBusy, profiles/valu_latest.json"),
+                         "build": provenance(vd, vp)}
         line = {
             "metric": "Ed25519 tx verifies/sec",
             "value": value,
@@ -638,6 +649,7 @@ def gpu_run(args, world, rank, local):
                        "execution": V.execution_settings()},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
+                         "traffic_build": traffic_build, "sources_sha256": digest,
                          "kernel": "verify_main_kernel (dominant: %.0f %% of the launch)"
                                    % (100.0 * main_ms / max(1e-9, sum(phase_ms.values()))),
                          "kernel_ms": main_ms, "work_per_verify": W_VERIFY, "units_per_launch": n,

@@ -192,9 +192,13 @@ int stl_tx_hash_batch_device(const uint8_t *d_preimages, const uint64_t *d_offse
  * Signature, TxnSignatures), which equals the reference's re-serialisation
  * when the blob is in canonical form; it checks that form and DEFERS every
  * blob it cannot prove canonical (stellard_amd/csrc/stl_txblob.h lists the
- * rules).  Blobs are assumed to be transactions the reference constructs
- * (template checks are the caller's, done when it built the object).
- * Per-transaction status: */
+ * rules).  It also restates the constructor's template checks
+ * (SerializedTransaction.cpp:79-91: TransactionType present with a TxFormats
+ * template, required fields present, no field outside the template), so
+ * STL_TX_OK implies the reference constructs the transaction; raw wire bytes
+ * are a safe input.  Validations (STL_BLOB_VALIDATION) with a field outside
+ * SerializedValidation's template are deferred (the reference drops such a
+ * field from the signing hash).  Per-transaction status: */
 #define STL_TX_OK 0        /* accept bit = checkSign(); tx_id valid */
 #define STL_TX_DEFERRED 1  /* accept bit 0; caller runs its own checkSign; tx_id zero */
 #define STL_TX_MALFORMED 2 /* SigningPubKey not 32 B or TxnSignature not 64 B: checkSign()

@@ -30,8 +30,12 @@
  *                                                 SerializedValidation.cpp:22-34,70-73,96-110,
  *                                                 HashPrefix.cpp:31; suppression
  *                                                 id SHA512Half(raw), PeerImp.cpp:1134,1148-1155
- * Not restated: the transaction-type templates (TxFormats.cpp, setType);
- * duplicate top-level fields are rejected as setType would reject them.
+ *   transactions: TransactionType present, a TxFormats template for it, and
+ *   setType's required / leftover checks   SerializedTransaction.cpp:79-91,
+ *                                          TxFormats.cpp:22-130,
+ *                                          SerializedObject.cpp:152-207,661-675
+ * Duplicate top-level fields are rejected as setType would reject them (the
+ * second one is a leftover).
  */
 #include <pthread.h>
 #include <stdlib.h>
@@ -470,6 +474,108 @@ static long vl_payload(const flist_t *l, uint32_t code, uint8_t *dst, size_t cap
   return -1;
 }
 
+/* TxFormats (TxFormats.cpp:22-111; addCommonFields :113-130): per TxType the
+ * template's fields with their SOElement flags. */
+enum { SOE_REQ = 0, SOE_OPT = 1, SOE_DEF = 2 };
+typedef struct {
+  uint32_t code;
+  int flags;
+} soe_t;
+static const soe_t kCommonFields[] = {
+    {0x10002u, SOE_REQ}, /* TransactionType */
+    {0x20002u, SOE_OPT}, /* Flags */
+    {0x20003u, SOE_OPT}, /* SourceTag */
+    {0x80001u, SOE_REQ}, /* Account */
+    {0x20004u, SOE_REQ}, /* Sequence */
+    {0x50005u, SOE_OPT}, /* PreviousTxnID */
+    {0x2001Bu, SOE_OPT}, /* LastLedgerSequence */
+    {0x50009u, SOE_OPT}, /* AccountTxnID */
+    {0x60008u, SOE_REQ}, /* Fee */
+    {0x2001Du, SOE_OPT}, /* OperationLimit */
+    {0xF0009u, SOE_OPT}, /* Memos */
+    {0x70003u, SOE_REQ}, /* SigningPubKey */
+    {0x70004u, SOE_OPT}, /* TxnSignature */
+};
+typedef struct {
+  int type;
+  soe_t f[6];
+  int n;
+} txformat_t;
+static const txformat_t kTxFormats[] = {
+    {3, {{0x2000Bu, SOE_OPT}, {0x20021u, SOE_OPT}, {0x20022u, SOE_OPT}, {0x80009u, SOE_OPT}, {0x8000Au, SOE_OPT}}, 5},
+    {4, {{0x80003u, SOE_REQ}, {0x2000Eu, SOE_OPT}}, 2},                                        /* AccountMerge */
+    {20, {{0x60003u, SOE_OPT}, {0x20014u, SOE_OPT}, {0x20015u, SOE_OPT}}, 3},                  /* TrustSet */
+    {7, {{0x60004u, SOE_REQ}, {0x60005u, SOE_REQ}, {0x2000Au, SOE_OPT}, {0x20019u, SOE_OPT}}, 4}, /* OfferCreate */
+    {8, {{0x20019u, SOE_REQ}}, 1},                                                             /* OfferCancel */
+    {5, {{0x80008u, SOE_OPT}}, 1},                                                             /* SetRegularKey */
+    {0,
+     {{0x80003u, SOE_REQ}, {0x60001u, SOE_REQ}, {0x60009u, SOE_OPT}, {0x120001u, SOE_DEF}, {0x50011u, SOE_OPT},
+      {0x2000Eu, SOE_OPT}},
+     6},                                                                                       /* Payment */
+    {1, {{0x2001Au, SOE_REQ}}, 1},                                                             /* Inflation */
+    {100, {{0x50013u, SOE_REQ}}, 1},                                                           /* EnableAmendment */
+    {101, {{0x30005u, SOE_REQ}, {0x2001Eu, SOE_REQ}, {0x2001Fu, SOE_REQ}, {0x20020u, SOE_REQ}}, 4}, /* SetFee */
+};
+
+/* one template element against the parsed list: SerializedObject.cpp:159-191 */
+static int soe_ok(const flist_t *l, const soe_t *e, uint8_t *used) {
+  for (size_t i = 0; i < l->n; ++i) {
+    if (used[i] || l->f[i].code != e->code) continue;
+    used[i] = 1;
+    /* SOE_DEFAULT present at its default: only sfPaths is SOE_DEFAULT, and an
+     * empty STPathSet cannot be deserialised (parse_value: "empty path") */
+    return 1;
+  }
+  return e->flags != SOE_REQ;
+}
+
+/* SerializedTransaction(SerializerIterator&) after set(): getFieldU16
+ * (SerializedObject.cpp:661-675), findByType, setType (SerializedObject.cpp:
+ * 152-207).  Leftover fields are never discardable: fieldValue is the wire
+ * name byte, at most 255 (FieldNames.h:178-181). */
+static int tx_template_ok(const flist_t *top) {
+  const fld_t *tf = NULL;
+  for (size_t i = 0; i < top->n && !tf; ++i)
+    if (top->f[i].code == 0x10002u) tf = &top->f[i];
+  if (!tf || tf->ser.n != 3) return 0; /* "Field not found" */
+  const int type = (tf->ser.p[1] << 8) | tf->ser.p[2];
+  const txformat_t *fmt = NULL;
+  for (size_t i = 0; i < sizeof kTxFormats / sizeof kTxFormats[0]; ++i)
+    if (kTxFormats[i].type == type) fmt = &kTxFormats[i];
+  if (!fmt) return 0; /* "invalid transaction type" */
+  uint8_t *used = (uint8_t *)calloc(top->n ? top->n : 1, 1);
+  int ok = 1;
+  for (size_t i = 0; i < sizeof kCommonFields / sizeof kCommonFields[0]; ++i) ok &= soe_ok(top, &kCommonFields[i], used);
+  for (int i = 0; i < fmt->n; ++i) ok &= soe_ok(top, &fmt->f[i], used);
+  for (size_t i = 0; i < top->n; ++i) ok &= used[i]; /* "invalid leftover" */
+  free(used);
+  return ok;
+}
+
+/* SerializedValidation's template (SerializedValidation.cpp:134-159).  Its
+ * constructor, STObject(getFormat(), sit, sfValidation), calls setType and
+ * ignores the result (SerializedObject.h:54-58): fields outside the template
+ * are dropped from the object (setType keeps only newData), so they are in
+ * neither the signing hash nor a re-serialisation; missing ones are simply
+ * absent. */
+static const uint32_t kValidationFields[] = {0x20002u,  0x50001u, 0x20006u, 0x20007u, 0x20018u, 0x130003u,
+                                             0x30005u,  0x2001Fu, 0x20020u, 0x20009u, 0x70003u, 0x70006u};
+
+static void validation_set_type(flist_t *top) {
+  size_t k = 0;
+  for (size_t i = 0; i < top->n; ++i) {
+    int keep = 0;
+    for (size_t j = 0; j < sizeof kValidationFields / sizeof kValidationFields[0]; ++j)
+      keep |= top->f[i].code == kValidationFields[j];
+    if (keep) {
+      top->f[k++] = top->f[i];
+    } else {
+      free(top->f[i].ser.p);
+    }
+  }
+  top->n = k;
+}
+
 int oracle_signed_blob(uint32_t kind, const uint8_t *blob, size_t len, uint8_t *signing, uint8_t *full,
                        size_t cap, oracle_txinfo *info) {
   memset(info, 0, sizeof *info);
@@ -481,12 +587,11 @@ int oracle_signed_blob(uint32_t kind, const uint8_t *blob, size_t len, uint8_t *
   flist_t top = {0};
   info->stopped_early = parse_object(&r, 0, &top) && r.pos < len ? 1 : 0;
   int rc = 0;
-  if (r.err || has_duplicates(&top)) rc = -1;
-  if (kind == 0) {
-    int has_type = 0;
-    for (size_t i = 0; i < top.n; ++i) has_type |= top.f[i].code == 0x10002u; /* getFieldU16(sfTransactionType) */
-    if (!has_type) rc = -1;
-  }
+  /* a duplicate is a setType leftover: fatal for a transaction, dropped for a
+   * validation (validation_set_type keeps both, add_sorted the first) */
+  if (r.err || (kind == 0 && has_duplicates(&top))) rc = -1;
+  if (kind == 0 && rc == 0 && !tx_template_ok(&top)) rc = -1;
+  if (kind == 1 && rc == 0) validation_set_type(&top);
   info->all_declared = r.all_declared;
   info->max_depth = r.max_depth;
   if (rc == 0) {

@@ -24,6 +24,18 @@ PRODUCT_DEPS = PRODUCT_SRCS + ["stl_kernels.h", "stl_verify_core.h", "stl_fe2551
                                os.path.join("..", "..", "include", "stl.h")]
 
 
+def source_digest():
+    """SHA-256 over the product's sources (PRODUCT_DEPS, in order): names the
+    build a profile was taken on, and lets bench.py tell whether the committed
+    profile summaries still describe the sources it runs."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in PRODUCT_DEPS:
+        with open(os.path.join(CSRC, d), "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
 def _stale(out, deps):
     if not os.path.exists(out):
         return True

@@ -822,6 +822,13 @@ int stl_init(const stl_config* cfg) {
   if (fa && *fa) g_fault_after.store(std::atoll(fa));
   g_trace = env_int("STL_TRACE", 0) != 0;
   if (env_int("STL_PHASE_TIMING", 0) != 0) g_phase_timing.store(true);
+  // execution tuning from the environment (same ranges as stl_debug_tuning;
+  // profiling runs use STL_STREAMS=1 so that kernels do not overlap)
+  {
+    const int s = env_int("STL_STREAMS", 0), c = env_int("STL_CHUNK_LOG2", 0);
+    if (s >= 1 && s <= (int)stl::kMaxVerifyStreams) g_tune_streams.store(s);
+    if (c >= 16 && c <= 20) g_tune_sub_log2.store(c);
+  }
   int first = 0, want = -1, spd = 1;
   uint32_t cflags = 0;
   if (cfg) {  // argument checks first: they need no device

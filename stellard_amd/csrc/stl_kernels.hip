@@ -250,6 +250,17 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_prep_ke
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
 
+// The value of the other lane of this lane's pair (lane ^ 1): one DPP move,
+// quad_perm [1,0,3,2] (dpp_ctrl 0xB1), a register-to-register swap inside the
+// VALU -- __shfl_xor lowers to ds_bpermute_b32, an LDS round trip per value.
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+#ifdef STL_PAIR_SHFL  // A/B only: the LDS permute the pair kernels used before
+  return (uint32_t)__shfl_xor((int)v, 1);
+#else
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+#endif
+}
+
 // verify_point_kernel for small chunks (the pair chunks of
 // verify_main_pair_kernel): lanes 2j and 2j+1 decode signature j's A and R,
 // one square-root chain each, swap the results and finish together; lane 0
@@ -278,10 +289,10 @@ __global__ __launch_bounds__(kBlock, 2) void verify_point_pair_kernel(
   const bool mok = phase1_decode_lane(mx, my, R, A, par);
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    ox.v[i] = (uint32_t)__shfl_xor((int)mx.v[i], 1);
-    oy.v[i] = (uint32_t)__shfl_xor((int)my.v[i], 1);
+    ox.v[i] = pair_swap(mx.v[i]);
+    oy.v[i] = pair_swap(my.v[i]);
   }
-  const bool ook = __shfl_xor((int)mok, 1) != 0;
+  const bool ook = pair_swap((uint32_t)mok) != 0;
   if (par == 0)
     phase1_points_finish_pair(h, R, S, A, core_policy(policy), mx, my, mok, ox, oy, ook);
   else
@@ -685,9 +696,9 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     verify_phase2_pair_chain(mine, h, par, tab, wl);
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-      other.X.v[i] = (uint32_t)__shfl_xor((int)mine.X.v[i], 1);
-      other.Y.v[i] = (uint32_t)__shfl_xor((int)mine.Y.v[i], 1);
-      other.Z.v[i] = (uint32_t)__shfl_xor((int)mine.Z.v[i], 1);
+      other.X.v[i] = pair_swap(mine.X.v[i]);
+      other.Y.v[i] = pair_swap(mine.Y.v[i]);
+      other.Z.v[i] = pair_swap(mine.Z.v[i]);
     }
     const bool ok = live && half_state_accepts(h) && pair_sums_cancel(mine, other);
     const uint64_t ball = __ballot(ok);
@@ -984,7 +995,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
           const uint32_t L = len[mi];
           bend = b + L;
           TxLayout t;
-          tx_blob_parse(b, L, t, kind.sig_code, kind.min_len);
+          tx_blob_parse(b, L, t, kind.sig_code, kind.min_len, kind.format);
           status[mi] = (uint8_t)t.status;
           uint4* sq = reinterpret_cast<uint4*>(sig + 64 * (size_t)mi);
           if (t.status == kTxOk) {

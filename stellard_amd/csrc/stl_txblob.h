@@ -33,7 +33,11 @@
 //     path elements with only the valid type bits, no empty path, and no
 //     account/issuer bit over a zero id (STPathElement recomputes the type
 //     from the ids, SerializedTypes.h:1179-1187);
-//   * length within [txMinSizeBytes, txMaxSizeBytes] (Protocol.h:41-45).
+//   * length within [txMinSizeBytes, txMaxSizeBytes] (Protocol.h:41-45);
+//   * transactions: the top level fits the TxFormats template of its
+//     TransactionType (tx_format below; SerializedTransaction.cpp:79-91);
+//     validations: no top-level field outside SerializedValidation's template
+//     (validation_field below: the reference drops such fields).
 // Amounts, integers, hashes and VL payloads re-serialise byte for byte from any
 // encoding the reference constructs (STAmount.cpp:465-560), so they need no
 // check beyond their size.
@@ -72,13 +76,120 @@ struct BlobKind {
   uint32_t id_prefix;    // ID = SHA512Half(id_prefix || blob), or of the blob alone
   uint32_t id_prefixed;  // 0: no prefix
   uint32_t min_len;
+  uint32_t format;       // top-level template check: kFormatTx or kFormatValidation
 };
+constexpr uint32_t kFormatNone = 0;        // no check (host tests of the bare pass)
+constexpr uint32_t kFormatTx = 1;          // TxFormats template of the TransactionType (tx_format)
+constexpr uint32_t kFormatValidation = 2;  // SerializedValidation's template (validation_field)
 // SerializedTransaction: checkSign / getTransactionID (SerializedTransaction.cpp:162-171,220-230)
-STL_HD BlobKind blob_kind_tx() { return BlobKind{kPrefixTxSign, kCodeTxnSignature, kPrefixTxId, 1u, kTxMinBytes}; }
+STL_HD BlobKind blob_kind_tx() { return BlobKind{kPrefixTxSign, kCodeTxnSignature, kPrefixTxId, 1u, kTxMinBytes, kFormatTx}; }
 // SerializedValidation::isValid (SerializedValidation.cpp:70-73,96-110); ID =
 // the suppression hash SHA512Half(raw validation), PeerImp.cpp:1148-1155
 STL_HD BlobKind blob_kind_validation() {
-  return BlobKind{kPrefixValidation, kCodeSignature, 0u, 0u, kValMinBytes};
+  return BlobKind{kPrefixValidation, kCodeSignature, 0u, 0u, kValMinBytes, kFormatValidation};
+}
+
+// ---- TxFormats templates (TxFormats.cpp:22-111, addCommonFields :113-130) ----
+// SerializedTransaction(SerializerIterator&) throws after set() unless
+// TransactionType is present (getFieldU16, SerializedObject.cpp:661-675), names
+// a format (findByType) and STObject::setType accepts the top-level fields
+// (SerializedObject.cpp:152-207): every SOE_REQUIRED field present, no field
+// outside the template (a leftover is discardable only with fieldValue > 256,
+// FieldNames.h:178-181, which no wire header can encode), no SOE_DEFAULT field
+// at its default (sfPaths: an empty path set, which the path-set walk already
+// defers).  Each template field has a bit; the masks below are the templates.
+STL_HD int tx_field_bit(uint32_t code) {
+  switch (code) {
+    case 0x10002u: return 0;   // TransactionType   (common fields)
+    case 0x20002u: return 1;   // Flags
+    case 0x20003u: return 2;   // SourceTag
+    case 0x80001u: return 3;   // Account
+    case 0x20004u: return 4;   // Sequence
+    case 0x50005u: return 5;   // PreviousTxnID
+    case 0x2001Bu: return 6;   // LastLedgerSequence
+    case 0x50009u: return 7;   // AccountTxnID
+    case 0x60008u: return 8;   // Fee
+    case 0x2001Du: return 9;   // OperationLimit
+    case 0xF0009u: return 10;  // Memos
+    case 0x70003u: return 11;  // SigningPubKey
+    case 0x70004u: return 12;  // TxnSignature
+    case 0x2000Bu: return 13;  // TransferRate      (AccountSet)
+    case 0x20021u: return 14;  // SetFlag
+    case 0x20022u: return 15;  // ClearFlag
+    case 0x80009u: return 16;  // InflationDest
+    case 0x8000Au: return 17;  // SetAuthKey
+    case 0x80003u: return 18;  // Destination       (AccountMerge, Payment)
+    case 0x2000Eu: return 19;  // DestinationTag
+    case 0x60003u: return 20;  // LimitAmount       (TrustSet)
+    case 0x20014u: return 21;  // QualityIn
+    case 0x20015u: return 22;  // QualityOut
+    case 0x60004u: return 23;  // TakerPays         (OfferCreate)
+    case 0x60005u: return 24;  // TakerGets
+    case 0x2000Au: return 25;  // Expiration
+    case 0x20019u: return 26;  // OfferSequence     (OfferCreate, OfferCancel)
+    case 0x80008u: return 27;  // RegularKey        (SetRegularKey)
+    case 0x60001u: return 28;  // Amount            (Payment)
+    case 0x60009u: return 29;  // SendMax
+    case 0x120001u: return 30; // Paths (SOE_DEFAULT)
+    case 0x50011u: return 31;  // InvoiceID
+    case 0x2001Au: return 32;  // InflateSeq        (Inflation)
+    case 0x50013u: return 33;  // Amendment         (EnableAmendment)
+    case 0x30005u: return 34;  // BaseFee           (SetFee)
+    case 0x2001Eu: return 35;  // ReferenceFeeUnits
+    case 0x2001Fu: return 36;  // ReserveBase
+    case 0x20020u: return 37;  // ReserveIncrement
+    default: return -1;
+  }
+}
+
+// SerializedValidation's template (SerializedValidation.cpp:134-159).  Its
+// constructor calls setType and ignores the result (SerializedObject.h:54-58):
+// a field outside the template is dropped from the object, so the signing
+// hash is not the splice of the blob -- such blobs are deferred.
+STL_HD bool validation_field(uint32_t code) {
+  switch (code) {
+    case 0x20002u:   // Flags
+    case 0x50001u:   // LedgerHash
+    case 0x20006u:   // LedgerSequence
+    case 0x20007u:   // CloseTime
+    case 0x20018u:   // LoadFee
+    case 0x130003u:  // Amendments
+    case 0x30005u:   // BaseFee
+    case 0x2001Fu:   // ReserveBase
+    case 0x20020u:   // ReserveIncrement
+    case 0x20009u:   // SigningTime
+    case 0x70003u:   // SigningPubKey
+    case 0x70006u:   // Signature
+      return true;
+    default:
+      return false;
+  }
+}
+
+STL_HD constexpr uint64_t tx_bits(int a, int b) { return ((2ull << b) - 1ull) & ~((1ull << a) - 1ull); }
+
+// allowed / required field bits of TxType `type`; false for a type TxFormats
+// does not define (findByType -> "invalid transaction type")
+STL_HD bool tx_format(uint32_t type, uint64_t& allowed, uint64_t& required) {
+  constexpr uint64_t kCommon = tx_bits(0, 12);
+  constexpr uint64_t kCommonReq = (1ull << 0) | (1ull << 3) | (1ull << 4) | (1ull << 8) | (1ull << 11);
+  uint64_t a, r;
+  switch (type) {
+    case 0: a = (1ull << 18) | (1ull << 19) | tx_bits(28, 31); r = (1ull << 18) | (1ull << 28); break;  // Payment
+    case 1: a = r = 1ull << 32; break;                                        // Inflation
+    case 3: a = tx_bits(13, 17); r = 0; break;                                // AccountSet
+    case 4: a = tx_bits(18, 19); r = 1ull << 18; break;                       // AccountMerge
+    case 5: a = 1ull << 27; r = 0; break;                                     // SetRegularKey
+    case 7: a = tx_bits(23, 26); r = tx_bits(23, 24); break;                  // OfferCreate
+    case 8: a = r = 1ull << 26; break;                                        // OfferCancel
+    case 20: a = tx_bits(20, 22); r = 0; break;                               // TrustSet
+    case 100: a = r = 1ull << 33; break;                                      // EnableAmendment
+    case 101: a = r = tx_bits(34, 37); break;                                 // SetFee
+    default: return false;
+  }
+  allowed = kCommon | a;
+  required = kCommonReq | r;
+  return true;
 }
 
 STL_HD uint64_t name_range(int a, int b) { return ((2ull << b) - 1ull) & ~((1ull << a) - 1ull); }
@@ -141,7 +252,7 @@ STL_HD bool bytes_nonzero(const uint8_t* b, uint32_t pos, uint32_t n) {
 // The canonical-form pass over one blob (one lane).  Byte loads only: fields
 // are short and the pass is a few percent of the hashing that follows.
 STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t, uint32_t sig_code = kCodeTxnSignature,
-                          uint32_t min_len = kTxMinBytes) {
+                          uint32_t min_len = kTxMinBytes, uint32_t format = kFormatTx) {
   t.status = kTxDeferred;
   t.pk_off = t.sig_off = 0;
   t.pk_len = t.sig_len = 0xffffffffu;
@@ -153,6 +264,9 @@ STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t, uint32_t 
   int depth = 0;
   int ncut = 0;
   bool cut_open = false;  // a cut TxnSignatures array still open
+  uint64_t present = 0;   // template bits of the top-level fields
+  bool foreign = false;   // a top-level field outside every template
+  uint32_t type_pos = 0;  // TransactionType payload
   uint32_t pos = 0;
   for (;;) {
     if (pos == len) {
@@ -199,6 +313,14 @@ STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t, uint32_t 
     }
     if (!field_declared(type, name) || code <= last[depth]) return;
     last[depth] = code;
+    if (depth == 0 && format == kFormatTx) {
+      const int fb = tx_field_bit(code);
+      if (fb < 0) foreign = true;
+      else present |= 1ull << fb;
+      if (code == 0x10002u) type_pos = pos;
+    } else if (depth == 0 && format == kFormatValidation && !validation_field(code)) {
+      foreign = true;
+    }
     const bool cut =
         depth == 0 && (code == kCodeTxnSignature || code == kCodeSignature || code == kCodeTxnSignatures);
     if (cut) {
@@ -274,6 +396,16 @@ STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t, uint32_t 
       else if (ncut == 2) t.xe1 = pos;
       else t.xe2 = pos;
     }
+  }
+  if (format == kFormatValidation && foreign) return;
+  if (format == kFormatTx) {
+    // the constructor's checks after set(): a blob that fails them never
+    // becomes a SerializedTransaction, so the device does not judge it
+    uint64_t allowed, required;
+    if (!(present & 1ull)) return;
+    const uint32_t tt = ((uint32_t)b[type_pos] << 8) | b[type_pos + 1];
+    if (foreign || !tx_format(tt, allowed, required)) return;
+    if ((present & ~allowed) != 0 || (required & ~present) != 0) return;
   }
   t.status = (t.pk_len == 32u && t.sig_len == 64u) ? kTxOk : kTxMalformed;
 }

@@ -263,7 +263,7 @@ void hostemu_signed_blob(uint32_t kind, const uint8_t* blob, uint32_t len, uint3
                          uint8_t id[32]) {
   const stl::BlobKind k = kind == 1 ? stl::blob_kind_validation() : stl::blob_kind_tx();
   stl::TxLayout t;
-  stl::tx_blob_parse(blob, len, t, k.sig_code, k.min_len);
+  stl::tx_blob_parse(blob, len, t, k.sig_code, k.min_len, k.format);
   *status = t.status;
   uint32_t h[8];
   std::memset(msg, 0, 32);

@@ -123,7 +123,13 @@ def test_fuzz_invariants(oracle, emu, corpus):
     built = 0
     for _ in range(4000):
         b = blobs[int(rng.integers(len(blobs)))]
-        m = T.mutate(rng, b)
+        if int(rng.integers(0, 10)) == 0:  # TxnSignature (optional) cut out: B12, checkSign false
+            i = b.index(b"\x74\x40")
+            m = b[:i] + b[i + 66:]
+            if int(rng.integers(0, 2)):
+                m = T.mutate(rng, m)
+        else:
+            m = T.mutate(rng, b)
         if int(rng.integers(0, 4)) == 0:
             m = T.mutate(rng, m)
         st, constructible = _check_device_vs_oracle(oracle, emu, m)
@@ -213,3 +219,54 @@ def test_device_pass_on_validations_and_fuzz(oracle, emu, val_corpus):
     # below PeerImp::recvValidation's 50-byte floor: deferred
     short = blobs[0][:49]
     assert hostemu_signed_blob(emu, VALIDATION, short)[0] == DEFERRED
+
+
+def test_validation_template_drops_foreign_fields(oracle, emu):
+    """SerializedValidation(sit) is STObject(getFormat(), sit, sfValidation):
+    set() then setType() with its result ignored (SerializedObject.h:54-58), so
+    a top-level field outside the validation template (SerializedValidation.cpp:
+    134-159) is dropped from the object and from the signing hash.  The oracle
+    restates that (a signature over the template fields alone verifies); the
+    device cannot splice such a blob and defers it; a duplicate template field
+    is dropped too (setType moves the first)."""
+    from tests.oracle_bind import hostemu_signed_blob
+    rng = np.random.default_rng(79)
+    pk, sk = oracle.keypair(rng.bytes(32))
+    for extra in ([T.Field(T.TransactionType, T.u16(0))], [T.Field(T.Memos, T.array_value(
+            [(T.Memo, [T.Field(T.MemoData, T.vl(b"hi"))])]))], [T.Field(T.TxnSignature, T.vl(bytes(64)))]):
+        fs = T.validation_fields(rng, pk)
+        h = h512half(T.validation_preimage(fs))
+        blob = T.serialize(fs + extra + [T.Field(T.Signature, T.vl(oracle.sign(h, sk)))])
+        ok, info, signing, full = oracle.signed_blob(VALIDATION, blob)
+        assert ok and signing == T.validation_preimage(fs) and full != blob
+        assert oracle.signed_blob_verify_batch(VALIDATION, [blob])[0].all()
+        assert hostemu_signed_blob(emu, VALIDATION, blob)[0] == DEFERRED
+        ref = load_sodium_ref()
+        if ref is not None:
+            from tests.oracle_bind import sodium_signed_blob_verify_batch
+            assert sodium_signed_blob_verify_batch(ref, VALIDATION, [blob]).all()
+    # the same validation without the extra field is decided on the device
+    fs = T.validation_fields(rng, pk)
+    blob, h, _ = T.signed_validation(fs, sk, oracle.sign)
+    assert hostemu_signed_blob(emu, VALIDATION, blob)[0] == OK
+
+
+def test_transaction_templates(oracle, emu):
+    """TxFormats (TxFormats.cpp:22-130) + SerializedTransaction's constructor
+    (SerializedTransaction.cpp:79-91): the device decides exactly the
+    constructible, canonical blobs of every transaction type; template
+    violations (missing required, foreign or duplicate fields, types without a
+    format) are unconstructible and deferred.  Covered case by case in
+    test_special_cases; here a sweep over every TransactionType value and
+    every template field added to a Payment."""
+    rng = np.random.default_rng(80)
+    pk, sk = oracle.keypair(rng.bytes(32))
+    base = T.payment_fields(rng, pk, 3)
+    rest = [x for x in base if x.fid != T.TransactionType]
+    decided = 0
+    for tt in list(range(0, 24)) + [99, 100, 101, 102, 255, 256, 0x7FFF, 0xFFFF]:
+        blob = T.signed_blob(rest + [T.Field(T.TransactionType, T.u16(tt))], sk, oracle.sign)[0]
+        st, constructible = _check_device_vs_oracle(oracle, emu, blob)
+        assert constructible == (tt == 0), tt  # Payment's fields fit no other template
+        decided += st != DEFERRED
+    assert decided == 1

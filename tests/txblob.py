@@ -36,6 +36,12 @@ Memos = (ARRAY, 9)
 TxnSignatures = (ARRAY, 3)
 Template = (ARRAY, 5)
 TakerPaysCurrency = (HASH160, 1)
+# fields of the other TxFormats templates (TxFormats.cpp:22-111)
+TakerPays, TakerGets = (AMOUNT, 4), (AMOUNT, 5)
+Expiration, OfferSequence, SetFlag = (UINT32, 10), (UINT32, 25), (UINT32, 33)
+QualityIn, InflateSeq, ReferenceFeeUnits = (UINT32, 20), (UINT32, 26), (UINT32, 30)
+RegularKey, InflationDest = (ACCOUNT, 8), (ACCOUNT, 9)
+Amendment = (HASH256, 19)
 # SerializedValidation's template (SerializedValidation.cpp:134-159)
 LedgerSequence, CloseTime, SigningTime = (UINT32, 6), (UINT32, 7), (UINT32, 9)
 LoadFee, ReserveBase, ReserveIncrement = (UINT32, 24), (UINT32, 31), (UINT32, 32)
@@ -85,6 +91,7 @@ def serialize(fields, sort=True, skip=()):
 # ------------------------------------------------------------- value encoders
 def u16(v): return int(v).to_bytes(2, "big")
 def u32(v): return int(v).to_bytes(4, "big")
+def u64(v): return int(v).to_bytes(8, "big")
 def vl(b): return vl_len(len(b)) + bytes(b)
 
 
@@ -267,10 +274,8 @@ def valid_corpus(oracle, n, seed, with_preimages=False, **kw):
                     paths=rng.random() < 0.25, extras=True)
         opts.update(kw)
         fs = payment_fields(rng, pk, i + 1, **opts)
-        if rng.random() < 0.1:  # a non-signing field besides TxnSignature (left out of the hash)
-            fs.append(Field(Signature, vl(rng.bytes(int(rng.integers(0, 80))))))
-        if rng.random() < 0.05:
-            fs.append(Field(TxnSignatures, array_value([((OBJECT, 2), [Field(SigningPubKey, vl(rng.bytes(32)))])])))
+        # (no top-level Signature / TxnSignatures: Payment's template has
+        # neither, so SerializedTransaction's constructor would throw)
         blob, _, _ = signed_blob(fs, sk, oracle.sign)
         blobs.append(blob)
         pres.append(signing_preimage(fs))
@@ -302,30 +307,71 @@ def special_cases(oracle, seed=7):
     out.append(("sig_63", serialize(base + [Field(TxnSignature, vl(sig[:63]))]), "malformed"))
     out.append(("sig_65", serialize(base + [Field(TxnSignature, vl(sig + b"\0"))]), "malformed"))
     out.append(("sig_missing", serialize(base), "malformed"))
-    f = [x for x in base if x.fid != SigningPubKey]
-    out.append(("pk_missing", serialize(f + [Field(TxnSignature, vl(sig))]), "malformed"))
-    # non-signing fields left out of the hash (Signature VL, TxnSignatures array), still valid
+    f = [x for x in base if x.fid != SigningPubKey]  # SOE_REQUIRED: the constructor throws
+    out.append(("pk_missing", serialize(f + [Field(TxnSignature, vl(sig))]), "unconstructible"))
+    # non-signing fields at the top level (Signature VL, TxnSignatures array):
+    # outside Payment's template, so the constructor throws (setType leftover)
     f = base + [Field(Signature, vl(b"xyz"))]
-    out.append(("with_Signature", signed_blob(f, sk, oracle.sign)[0], "ok"))
+    out.append(("with_Signature", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
     f = base + [Field(TxnSignatures, array_value([((OBJECT, 2), [Field(SigningPubKey, vl(bytes(33)))])]))]
-    out.append(("with_TxnSignatures", signed_blob(f, sk, oracle.sign)[0], "ok"))
-    f = base + [Field(Signature, vl(b"")),
-                Field(TxnSignatures, array_value([((OBJECT, 2), [Field(Sequence, u32(1)), Field(Fee, amount_native(1))])]))]
-    out.append(("with_both", signed_blob(f, sk, oracle.sign)[0], "ok"))
-    # nested objects and arrays (canonical), path sets, vector256
+    out.append(("with_TxnSignatures", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
+    # ---- TxFormats templates (TxFormats.cpp:22-130, setType SerializedObject.cpp:152-207)
+    def without(fields, fid):
+        return [x for x in fields if x.fid != fid]
+    out.append(("payment_no_amount", signed_blob(without(base, Amount), sk, oracle.sign)[0], "unconstructible"))
+    out.append(("payment_no_destination", signed_blob(without(base, Destination), sk, oracle.sign)[0],
+                "unconstructible"))
+    out.append(("payment_no_fee", signed_blob(without(base, Fee), sk, oracle.sign)[0], "unconstructible"))
+    out.append(("no_sequence", signed_blob(without(base, Sequence), sk, oracle.sign)[0], "unconstructible"))
+    out.append(("no_account", signed_blob(without(base, Account), sk, oracle.sign)[0], "unconstructible"))
+    out.append(("no_transaction_type", signed_blob(without(base, TransactionType), sk, oracle.sign)[0],
+                "unconstructible"))
+    f = base + [Field(TakerPays, amount_native(5))]  # an OfferCreate field in a Payment
+    out.append(("payment_foreign_field", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
+    f = base + [Field(Hashes, vl(rng.bytes(64)))]  # declared, in no transaction template
+    out.append(("payment_vector256", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
+    for tt in (2, 6, 9, 10, 99, 102, 0xFFFF):  # WalletAdd, NicknameSet, Contract(Remove): no format
+        f = without(base, TransactionType) + [Field(TransactionType, u16(tt))]
+        out.append((f"type_{tt}_no_format", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
+    common = without(without(without(base, TransactionType), Amount), Destination)
+    typed = {
+        "offer_create": (7, [Field(TakerPays, amount_native(5)), Field(TakerGets, amount_native(7)),
+                             Field(Expiration, u32(9)), Field(OfferSequence, u32(3))]),
+        "offer_cancel": (8, [Field(OfferSequence, u32(3))]),
+        "account_set": (3, [Field(SetFlag, u32(1)), Field(InflationDest, vl(rng.bytes(20)))]),
+        "account_merge": (4, [Field(Destination, vl(rng.bytes(20)))]),
+        "trust_set": (20, [Field(QualityIn, u32(1))]),
+        "regular_key": (5, [Field(RegularKey, vl(rng.bytes(20)))]),
+        "inflation": (1, [Field(InflateSeq, u32(11))]),
+        "amendment": (100, [Field(Amendment, rng.bytes(32))]),
+        "set_fee": (101, [Field(BaseFee, u64(10)), Field(ReferenceFeeUnits, u32(10)), Field(ReserveBase, u32(20)),
+                          Field(ReserveIncrement, u32(5))]),
+    }
+    for name, (tt, extra) in typed.items():
+        f = common + [Field(TransactionType, u16(tt))] + extra
+        out.append((name, signed_blob(f, sk, oracle.sign)[0], "ok"))
+        if any(True for _ in extra):  # drop the first field: required ones make it unconstructible
+            req = name in ("offer_create", "offer_cancel", "account_merge", "inflation", "amendment", "set_fee")
+            f = common + [Field(TransactionType, u16(tt))] + extra[1:]
+            out.append((name + "_minus_first", signed_blob(f, sk, oracle.sign)[0], "unconstructible" if req else "ok"))
+    f = common + [Field(TransactionType, u16(7)), Field(TakerPays, amount_native(5)), Field(TakerGets, amount_native(7)),
+                  Field(Amount, amount_native(1))]
+    out.append(("offer_with_amount", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
+    # nested objects and arrays (canonical), path sets, vector256 (inside a
+    # Memo: inner objects have no template)
     out.append(("memos", signed_blob(fs0(memos=3), sk, oracle.sign)[0], "ok"))
     out.append(("paths", signed_blob(fs0(paths=True), sk, oracle.sign)[0], "ok"))
-    f = base + [Field(Hashes, vl(rng.bytes(64)))]
+    f = base + [Field(Memos, array_value([(Memo, [Field(Hashes, vl(rng.bytes(64)))])]))]
     out.append(("vector256", signed_blob(f, sk, oracle.sign)[0], "ok"))
     deep = [Field(MemoData, vl(b"x"))]
-    for _ in range(4):  # (ARRAY > element object) x 4: fields at depth 8, the deepest the device takes
+    for _ in range(3):  # (ARRAY > element object) x 4: fields at depth 8, the deepest the device takes
         deep = [Field(Template, array_value([(TemplateEntry, deep)]))]
-    f = base + deep
+    f = base + [Field(Memos, array_value([(Memo, deep)]))]
     out.append(("depth_ok", signed_blob(f, sk, oracle.sign)[0], "ok"))
     deep = [Field(MemoData, vl(b"x"))]
-    for _ in range(5):
+    for _ in range(4):
         deep = [Field(Template, array_value([(TemplateEntry, deep)]))]
-    f = base + deep
+    f = base + [Field(Memos, array_value([(Memo, deep)]))]
     out.append(("depth_too_deep", signed_blob(f, sk, oracle.sign)[0], "defer"))
     # long VL encodings (2- and 3-byte lengths)
     f = base + [Field(Memos, array_value([(Memo, [Field(MemoData, vl(rng.bytes(300)))])]))]
@@ -344,7 +390,7 @@ def special_cases(oracle, seed=7):
     f = base + [Field(Memos, array_value([(Memo, inner)], sort=False))]
     out.append(("inner_order", serialize(f + [Field(TxnSignature, vl(oracle.sign(sha512_half(
         b"STX\x00" + serialize(f, skip=NON_SIGNING)), sk)))]), "defer"))
-    f = base + [Field(Hashes, vl(rng.bytes(40)))]  # Vector256 with a partial entry
+    f = base + [Field(Memos, array_value([(Memo, [Field(Hashes, vl(rng.bytes(40)))])]))]  # partial Vector256 entry
     out.append(("vector256_partial", signed_blob(f, sk, oracle.sign)[0], "defer"))
     f = base + [Field(Paths, b"\x01" + b"\0" * 20 + b"\x00")]  # account bit over a zero account
     out.append(("path_zero_account", signed_blob(f, sk, oracle.sign)[0], "defer"))
@@ -355,8 +401,10 @@ def special_cases(oracle, seed=7):
     f = base + [Field(Paths, b"\x02" + b"\x00")]
     out.append(("path_bad_type", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
     # undeclared field of a known type: the reference makes one up; the device defers
-    f = base + [Field((UINT32, 60), u32(1))]
+    f = base + [Field(Memos, array_value([(Memo, [Field((UINT32, 60), u32(1))])]))]
     out.append(("dynamic_field", signed_blob(f, sk, oracle.sign)[0], "defer"))
+    f = base + [Field((UINT32, 60), u32(1))]  # at the top level it is a setType leftover
+    out.append(("dynamic_field_top", signed_blob(f, sk, oracle.sign)[0], "unconstructible"))
     # array left open at the end of the blob (re-serialisation adds 0xF1)
     f = base + [Field(TxnSignature, vl(sig))]
     out.append(("array_unterminated", serialize(f) + field_id(*Memos) + field_id(*Memo) + b"\xe1", "defer"))

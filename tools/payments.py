@@ -12,7 +12,7 @@ def payment_preimages(pks, n, rng, pad_lens=None):
     """Signing preimages "STX\\0" || Payment fields without TxnSignature
     (Account/Destination are synthetic 20-byte ids).
     pad_lens: optional target preimage lengths (config 5) reached with a
-    Memo-like VL field."""
+    Memos array holding one MemoData."""
     out = []
     nacc = pks.shape[0]
     seq = np.zeros(nacc, np.int64)
@@ -33,14 +33,16 @@ def payment_preimages(pks, n, rng, pad_lens=None):
             f += b"\x61" + head.to_bytes(8, "big") + b"\0" * 12 + b"USD" + b"\0" * 5 + rng.bytes(20)
         f += b"\x68" + (10 | 0x4000000000000000).to_bytes(8, "big")  # Fee
         f += b"\x73\x20" + pks[a].tobytes()                    # SigningPubKey
-        if pad_lens is not None:
-            want = int(pad_lens[i]) - len(f) - 44
-            if want > 196:
-                body = rng.bytes(min(want - 3, 12480))
-                v = len(body) - 193                            # VL length, 2-byte form
-                f += b"\x7d" + bytes([193 + (v >> 8), v & 0xff]) + body  # Memo-like VL padding
         f += b"\x81\x14" + hashlib.sha256(pks[a].tobytes()).digest()[:20]  # Account
         f += b"\x83\x14" + rng.bytes(20)                                   # Destination
+        if pad_lens is not None:
+            # Memos [ Memo { MemoData } ]: the one array Payment's template
+            # allows (TxFormats.cpp:113-130), last in fieldCode order
+            want = int(pad_lens[i]) - len(f)
+            if want > 200:
+                body = rng.bytes(min(want - 7, 12480))
+                v = len(body) - 193                            # VL length, 2-byte form
+                f += b"\xf9\xea\x7d" + bytes([193 + (v >> 8), v & 0xff]) + body + b"\xe1\xf1"
         out.append(bytes(f))
     return out
 

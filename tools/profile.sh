@@ -9,7 +9,11 @@ set -euo pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-prof}
 mkdir -p $OUT
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
+# STL_STREAMS=1: each verify call runs its kernels one after another on one
+# stream (1M-signature chunks), so every kernel's duration and counters are its
+# own -- the launches the bench's phase clock times
+export STL_STREAMS=1 STL_EXEC_NOTE="STL_STREAMS=1 (kernels serial, 2^20-signature chunks)"
+B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extra"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $B > $OUT/trace_bench.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- $B > $OUT/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- $B > $OUT/pmc_write.log 2>&1

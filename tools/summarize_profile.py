@@ -70,6 +70,10 @@ if "--traffic" in sys.argv:
                "hbm_bytes_per_launch": tot["hbm_bytes_per_launch"],
                "hbm_bytes_per_launch_fetch_x2_upper": tot["hbm_bytes_per_launch_fetch_x2_upper"],
                "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, raw; FETCH x2 (gfx950 wide-read correction) upper bound"}
+    sys.path.insert(0, ROOT)
+    from stellard_amd.build import source_digest
+    traffic["build"] = {"sources_sha256": source_digest(), "git_head": os.environ.get("GIT_HEAD"),
+                        "execution": os.environ.get("STL_EXEC_NOTE")}
     m = summary["kernels"].get("stl::verify_main_kernel")
     if m:  # the dominant kernel, as bench.py's roofline reports it
         traffic["main_kernel"] = {

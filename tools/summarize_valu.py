@@ -41,7 +41,12 @@ def main():
     k = load(d)
     w = sum(v.get("GRBM_GUI_ACTIVE", 0) for v in k.values())
     busy = sum(v.get("VALUBusy", 0) * v.get("GRBM_GUI_ACTIVE", 0) for v in k.values()) / w if w else None
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from stellard_amd.build import source_digest
     doc = {"source": d + " (rocprofv3 --pmc, one pass per counter group: tools/valu_pmc.sh)",
+           "build": {"sources_sha256": source_digest(), "git_head": os.environ.get("GIT_HEAD"),
+                     "execution": os.environ.get("STL_EXEC_NOTE")},
            "launch_valu_busy_pct": busy, "kernels": k}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)

@@ -6,7 +6,11 @@ set -euo pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-valu}
 mkdir -p $OUT
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
+# STL_STREAMS=1: each verify call runs its kernels one after another on one
+# stream (1M-signature chunks), so every kernel's duration and counters are its
+# own -- the launches the bench's phase clock times
+export STL_STREAMS=1 STL_EXEC_NOTE="STL_STREAMS=1 (kernels serial, 2^20-signature chunks)"
+B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extra"
 pass() {
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT/$name -o run --output-format csv -- $B > $OUT/$name.log 2>&1
@@ -16,4 +20,4 @@ pass busy VALUBusy
 pass util VALUUtilization
 pass occ OccupancyPercent
 pass mocc MeanOccupancyPerActiveCU
-echo valu-pmc-done
+python3 tools/summarize_valu.py $OUT > $OUT/summary.log && echo valu-pmc-done
