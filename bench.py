@@ -73,7 +73,8 @@ def parse():
                          "rehearsal of the multi-rank flow with every rank on the visible GPU(s), e.g. 2 ranks on "
                          "a 1-GPU box (RCCL refuses two ranks on one device)")
     ap.add_argument("--no-extra", action="store_true",
-                    help="skip the configs[2] / configs[4] legs reported under extra_configs")
+                    help="skip the configs[2] / configs[4] / config-1 legs and the end_to_end leg (profiling runs: "
+                         "only the bench batch's own launches are traced)")
     return ap.parse_args()
 
 
@@ -669,7 +670,7 @@ def gpu_run(args, world, rank, local):
                       "verifies": n * args.steps},
             "extra_configs": extra,
         }
-        if world == 1:
+        if world == 1 and not args.no_extra:
             try:
                 line["end_to_end"] = end_to_end(V, torch, sig, msgs, pk)
             except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench line
