@@ -447,7 +447,7 @@ int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode,
   x.wide = static_cast<const uint4*>(d.wide.p);
   x.counters = dev_counters(d);
   x.clock = phase_clock(d);
-  x.fused_prep = g_tune_fused.load() != 0;
+  x.fused_prep = g_tune_fused.load();
   x.main_queue = g_tune_queue.load() != 0;
   x.sub = 1u << g_tune_sub_log2.load();
   uint32_t S = (uint32_t)std::max(1, std::min<int>(streams, (int)stl::kMaxVerifyStreams));
@@ -942,7 +942,7 @@ int stl_debug_tuning(int key, int value) {
   }
   switch (key) {
     case STL_TUNE_FUSED_PREP:
-      if (value != 0 && value != 1) return STL_EINVAL;
+      if (value < 0 || value > 2) return STL_EINVAL;
       return g_tune_fused.exchange(value);
     case STL_TUNE_MAIN_QUEUE:
       if (value != 0 && value != 1) return STL_EINVAL;

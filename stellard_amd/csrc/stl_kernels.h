@@ -86,7 +86,8 @@ struct VerifyExec {
   const uint4* wide = nullptr;          // wide base tables
   unsigned long long* counters = nullptr;
   const PhaseClock* clock = nullptr;
-  bool fused_prep = true;               // scalar + point half of phase 1 in one kernel
+  int fused_prep = 1;                   // 0: scalar and point kernels; 1: phase 1 in one kernel;
+                                        // 2: phase 1 inside the main kernel (verify_whole_kernel)
   bool main_queue = true;               // main kernel pulls 64-signature units from a counter
   uint32_t nstreams = 1;
   uint32_t sub = kPreChunk;             // chunk size when nstreams > 1 (multiple of 64, >= 2^16)

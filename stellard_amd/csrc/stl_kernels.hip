@@ -238,6 +238,28 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_prep_ke
   load_k(k, R, A, msg_or_k, j, PRE_K);
   HalfState h;
   verify_phase1_scalars(h, S, k);
+#ifdef STL_PREP_EARLY_STORE
+  // the scalar half's digits leave the registers before the square-root
+  // chains (only `tops` stays live); quad 2 is rewritten with the final flags
+  uint4* q = pre + (size_t)tt * 14;
+  {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < kHalfScalarQuads; ++i)
+        st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+    }
+  }
+  verify_phase1_points(h, R, S, A, core_policy(policy));
+  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  if (live) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
+    st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
+#pragma unroll
+    for (int i = kHalfScalarQuads; i < 14; ++i)
+      st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+  }
+#else
   verify_phase1_points(h, R, S, A, core_policy(policy));
   if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
   if (live) {
@@ -246,6 +268,7 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_prep_ke
 #pragma unroll
     for (int i = 0; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
   }
+#endif
   const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
@@ -662,6 +685,73 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const bool ok = verify_phase2_half(h, tab1, tab2, wl, keytabs, widetabs) && live;
     const uint64_t word = __ballot(ok);
     if (lane == 0) {
+      bitmap[(base + wbase) >> 6] = word;
+      if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popcll(word));  // accepted (stl_get_stats)
+    }
+    if (!queue) unit += stride;
+  }
+}
+
+// Phase 1 and phase 2 in one kernel (STL_TUNE_FUSED_PREP 2): a wave takes a
+// 64-signature unit and runs verify_prep_kernel's work on it (k, half-size
+// scalars, pre-checks, decodings) and then the Straus loop, with the phase-1
+// state in registers -- no 224-B HalfState write and read per signature and
+// one kernel boundary per chunk.  The decodings run at the main kernel's
+// occupancy (2 waves/SIMD, no spills) instead of 4 waves with spills.  The
+// fallback flags go to fb_words for verify_fallback_kernel, as phase 1's do.
+template <bool PRE_K>
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_whole_kernel(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
+    uint32_t base, uint32_t cnt, uint32_t policy, uint64_t* __restrict__ fb_words, uint64_t* __restrict__ bitmap,
+    uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
+    uint32_t* __restrict__ queue) {
+  TableView tab1, tab2;
+  lane_tables(ws, tab1, tab2);
+  __shared__ uint4 tails[18][kBlock];
+  tab1.tail = &tails[0][threadIdx.x];
+  tab2.tail = &tails[9][threadIdx.x];
+  tab1.tstride = tab2.tstride = kBlock;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  WideGlobal wl{wide, {0, 0}};
+  const uint32_t units = (cnt + 63) >> 6;
+  const uint32_t stride = gridDim.x * (kBlock / 64);
+  uint32_t unit = blockIdx.x * (kBlock / 64) + wave;
+  for (;;) {
+    if (queue) {  // wave-uniform: one atomic per wave and unit
+      uint32_t u = 0;
+      if (lane == 0) u = atomicAdd(queue, 1u);
+      unit = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+    }
+    if (unit >= units) break;
+    const uint32_t wbase = unit * 64;
+    const uint32_t t = wbase + lane;
+    const bool live = t < cnt;
+    const size_t j = (size_t)base + (live ? t : cnt - 1);
+    HalfState h;
+    {
+      uint32_t R[8], S[8], A[8], k[8];
+      ld8(R, sig + 64 * j);
+      ld8(S, sig + 64 * j + 32);
+      ld8(A, pk + 32 * j);
+      load_k(k, R, A, msg_or_k, j, PRE_K);
+      verify_phase1_scalars(h, S, k);
+#ifdef STL_WHOLE_PAIRED  // the two square-root chains interleaved (more ILP, more registers)
+      const uint32_t pol = core_policy(policy);
+      const bool pre_ok = verify_prechecks(R, S, A, pol) && composite_s_ok(S, pol) && r_is_canonical(R);
+      ge_p3 negA, negQ;
+      bool okA, okR;
+      ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
+      finish_phase1_points(h, negA.X, negA.Y, negQ.X, negQ.Y, pre_ok && okA && okR);
+#else
+      verify_phase1_points(h, R, S, A, core_policy(policy));
+#endif
+    }
+    if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+    const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
+    const bool ok = verify_phase2_half(h, tab1, tab2, wl) && live;
+    const uint64_t word = __ballot(ok);
+    if (lane == 0) {
+      fb_words[wbase >> 6] = fb;
       bitmap[(base + wbase) >> 6] = word;
       if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popcll(word));  // accepted (stl_get_stats)
     }
@@ -1194,7 +1284,28 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
 #endif
     const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
-    const bool fused = x.fused_prep && !pair_point && !dedup;
+    if (x.fused_prep == 2 && !pair && !dedup) {
+      // the whole verification in one kernel (phase clock: all of it is "main")
+      mark(0);
+      mark(1);
+      mark(2);
+      if (pre_k)
+        hipLaunchKernelGGL(verify_whole_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
+                           policy, fb, bitmap, slots, wide, counters, qctr);
+      else
+        hipLaunchKernelGGL(verify_whole_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
+                           policy, fb, bitmap, slots, wide, counters, qctr);
+      mark(3);
+      if (pre_k)
+        hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
+                           policy, fb, bitmap, slots, counters);
+      else
+        hipLaunchKernelGGL(verify_fallback_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
+                           policy, fb, bitmap, slots, counters);
+      mark(4);
+      return hipGetLastError();
+    }
+    const bool fused = x.fused_prep != 0 && !pair_point && !dedup;
     mark(0);
     if (fused && pre_k)
       hipLaunchKernelGGL(verify_prep_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
