@@ -238,9 +238,10 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_prep_ke
   load_k(k, R, A, msg_or_k, j, PRE_K);
   HalfState h;
   verify_phase1_scalars(h, S, k);
-#ifdef STL_PREP_EARLY_STORE
   // the scalar half's digits leave the registers before the square-root
-  // chains (only `tops` stays live); quad 2 is rewritten with the final flags
+  // chains (only `tops` stays live); quad 2 is rewritten with the final flags.
+  // Same-box A/B: -0.3 % per launch against storing all 14 quads at the end
+  // (profiles/r03/c).
   uint4* q = pre + (size_t)tt * 14;
   {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
@@ -259,16 +260,6 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_prep_ke
     for (int i = kHalfScalarQuads; i < 14; ++i)
       st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
   }
-#else
-  verify_phase1_points(h, R, S, A, core_policy(policy));
-  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
-  if (live) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
-    uint4* q = pre + (size_t)t * 14;
-#pragma unroll
-    for (int i = 0; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
-  }
-#endif
   const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }

@@ -170,24 +170,30 @@ STL_HD void load_base_niels(ge_niels& n, const uint32_t* tab, int absd) {
   fe_cmov(n.xy2d, n.xy2d, id.xy2d, z);
 }
 
-// Per-lane table of cached multiples e*P, e = 0..8 (entry 0 = identity).
+// Per-lane table of cached multiples e*P, e = 0..8 (entry 0 = identity), for
+// an AFFINE P (Z = 1, T = xy -- every caller's P comes from a decoding or
+// affine_to_p3): P's cached form is then its Niels form (Y+X, Y-X, 2dT with
+// Z = 1), so 3P..8P are mixed additions (ge_madd, one product fewer than
+// ge_add_cached) and 2P skips the square of Z.
 STL_HD void build_cached_table(const TableView& tab, const ge_p3& P) {
   ge_cached c1, c;
   ge_cached_0(c);
   tab.store(0, c);
   ge_p3_to_cached(c1, P);
   tab.store(1, c1);
+  ge_niels n1;
+  n1.ypx = c1.YpX;
+  n1.ymx = c1.YmX;
+  n1.xy2d = c1.T2d;
   ge_p1p1 t;
-  ge_p2 p2;
   ge_p3 p3;
-  ge_p3_to_p2(p2, P);
-  ge_p2_dbl(t, p2);
+  ge_affine_dbl(t, P);
   ge_p1p1_to_p3(p3, t);
   ge_p3_to_cached(c, p3);
   tab.store(2, c);
 #pragma unroll 1
   for (int e = 3; e <= 8; ++e) {
-    ge_add_cached(t, p3, c1);
+    ge_madd(t, p3, n1);
     ge_p1p1_to_p3(p3, t);
     ge_p3_to_cached(c, p3);
     tab.store(e, c);
