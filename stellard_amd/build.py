@@ -77,10 +77,18 @@ def build_oracle():
 
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
-    build_product(force="--force" in argv)
-    if "--product-only" not in argv:
-        build_hostemu(force="--force" in argv)
-        build_oracle()
+    force = "--force" in argv
+    if "--product-only" in argv:
+        build_product(force=force)
+        return
+    # the product and the host harness are independent single-threaded
+    # compiles of the same device code: run them side by side
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        jobs = [ex.submit(build_product, force), ex.submit(build_hostemu, force)]
+        for j in jobs:
+            j.result()
+    build_oracle()
 
 
 if __name__ == "__main__":
