@@ -22,35 +22,19 @@ sys.path.insert(0, ROOT)
 
 
 def make_blobs(n, seed, uniform=0):
-    """Payment-shaped blobs: fixed fields, a MemoData pad to the target length
-    (log-uniform 100 B - 4 KB, or all `uniform` bytes)."""
+    """Payment transactions (tools/payments.py: the Payment template, a Memos
+    array as the pad) with preimage lengths log-uniform in 100 B - 4 KB, or
+    all `uniform` bytes: (signing preimages, serialized transactions)."""
+    from tools.payments import blobs_from_preimages, payment_preimages
     rng = np.random.default_rng(seed)
     target = np.exp(rng.uniform(np.log(100), np.log(4096), n)).astype(np.int64)
     if uniform:
         target[:] = uniform
-    head = (b"\x12\x00\x00" + b"\x22\x80\x00\x00\x00" + b"\x24\x00\x00\x00\x01" +
-            b"\x61" + (123456 | 0x4000000000000000).to_bytes(8, "big") +
-            b"\x68" + (10 | 0x4000000000000000).to_bytes(8, "big"))
-    rand = rng.bytes(n * 64 + 4096 * 4)
-    pres, blobs = [], []
-    for i in range(n):
-        r = rand[64 * i:64 * i + 64]
-        pk = r[:32]
-        tail = b"\x81\x14" + r[32:52] + b"\x83\x14" + r[44:64]
-        body = head + b"\x73\x20" + pk
-        pad = int(target[i]) - (len(body) + len(tail) + 66)
-        memo = b""
-        if pad > 3:
-            m = min(pad - 3, 12480)
-            if m <= 192:
-                memo = b"\x7d" + bytes([m]) + rand[i % 4096:i % 4096 + m]
-            else:
-                v = m - 193
-                memo = b"\x7d" + bytes([193 + (v >> 8), v & 0xFF]) + rand[i % 4096:i % 4096 + m]
-        sig = rand[(64 * i + 7) % (64 * n): (64 * i + 7) % (64 * n) + 64].ljust(64, b"\1")
-        pres.append(b"STX\x00" + body + memo + tail)
-        blobs.append(body + b"\x74\x40" + sig + memo + tail)
-    return pres, blobs
+    pks = np.frombuffer(rng.bytes(1000 * 32), np.uint8).reshape(1000, 32)
+    pres = payment_preimages(pks, n, rng, pad_lens=target)
+    sig = np.frombuffer(rng.bytes(n * 64), np.uint8).reshape(n, 64)
+    pk = pks[np.arange(n) % 1000]
+    return pres, blobs_from_preimages(pres, sig, pk)
 
 
 def pack(chunks):
