@@ -325,6 +325,84 @@ __global__ __launch_bounds__(kBlock, 2) void verify_point_pair_kernel(
   if ((threadIdx.x & 63u) == 0 && (wsig >> 6) < ((cnt + 63) >> 6)) reinterpret_cast<uint32_t*>(fb_words)[wsig >> 5] = half;
 }
 
+// Phase 1 of the lane-pair path (chunks that run verify_main_pair_kernel) as
+// ONE launch whose workgroups take one of two roles, so the scalar half
+// (SHA-512, lattice: a latency-bound chain) and the two square-root chains run
+// side by side on different CUs instead of one launch after the other -- a
+// small batch leaves most of the chip idle, so the phase costs the longer of
+// the two chains, not their sum:
+//   blocks [0, nbs)         scalar role, one lane per signature: quads 0-3
+//                           and words 16-18 of the HalfState (digits, tops
+//                           with the c / d signs and the fit flag);
+//   blocks [nbs, gridDim)   point role, two lanes per signature (lane 2j
+//                           decodes A, 2j+1 decodes R, one DPP swap): lane 0
+//                           stores -A and -Q raw in quads 5-13 and word 19 =
+//                           pre-checks && both decodings (kPairPointOk).
+// The two roles write disjoint words; verify_main_pair_kernel combines them
+// (finish_phase1_points, as the split kernels do) and writes the fallback
+// words.
+constexpr uint32_t kPairPointOk = 1u;
+template <bool PRE_K>
+__global__ __launch_bounds__(kBlock, 2) void verify_prep_pair_kernel(
+    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
+    uint32_t base, uint32_t cnt, uint32_t policy, uint4* __restrict__ pre, uint32_t nbs) {
+  if (blockIdx.x < nbs) {  // scalar role (workgroup-uniform)
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= cnt) return;  // no wave-level collective in this role
+    const size_t j = (size_t)base + t;
+    uint32_t R[8], S[8], A[8], k[8];
+    ld8(R, sig + 64 * j);
+    ld8(S, sig + 64 * j + 32);
+    ld8(A, pk + 32 * j);
+    load_k(k, R, A, msg_or_k, j, PRE_K);
+    HalfState h;
+    verify_phase1_scalars(h, S, k);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
+    uint4* q = pre + (size_t)t * 14;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+    uint32_t* q4 = reinterpret_cast<uint32_t*>(q + 4);  // words 16-18; word 19 is the point role's
+    q4[0] = w[16];
+    q4[1] = w[17];
+    q4[2] = w[18];
+    return;
+  }
+  const uint32_t g = (blockIdx.x - nbs) * kBlock + threadIdx.x;  // point role
+  const uint32_t t = g >> 1;
+  const int par = (int)(g & 1u);
+  const bool live = t < cnt;
+  const uint32_t tt = live ? t : cnt - 1;
+  const size_t j = (size_t)base + tt;
+  uint32_t R[8], A[8];
+  ld8(R, sig + 64 * j);
+  ld8(A, pk + 32 * j);
+  fe mx, my, ox, oy;
+  const bool mok = phase1_decode_lane(mx, my, R, A, par);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    ox.v[i] = pair_swap(mx.v[i]);
+    oy.v[i] = pair_swap(my.v[i]);
+  }
+  const bool ook = pair_swap((uint32_t)mok) != 0;
+  if (live && par == 0) {  // lane 0 holds A's decoding in m, R's in o
+    uint32_t S[8];
+    ld8(S, sig + 64 * j + 32);
+    const uint32_t pol = core_policy(policy);
+    const bool ok = verify_prechecks(R, S, A, pol) && composite_s_ok(S, pol) && r_is_canonical(R) && mok && ook;
+    HalfState h;
+    h.P1x = mx;
+    h.P1y = my;
+    h.P2x = ox;
+    h.P2y = oy;
+    h.pad = ok ? kPairPointOk : 0u;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
+    uint4* q = pre + (size_t)t * 14;
+    reinterpret_cast<uint32_t*>(q + 4)[3] = w[19];
+#pragma unroll
+    for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+  }
+}
+
 // ---- per-batch key dedup (STL_DEDUP_KEYS) ----
 // stellard's signers repeat (configs 1 and 5: 1,000 accounts for 100k
 // transactions), so the batch decodes each distinct key once:
@@ -757,8 +835,9 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
 // even bits of its ballot are one 32-bit half of a bitmap word (the other
 // half is the next wave's, in the same tile).
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_pair_kernel(
-    const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
-    uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr) {
+    const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint32_t policy, uint64_t* __restrict__ bitmap,
+    uint64_t* __restrict__ fb_words, uint4* __restrict__ ws, const uint4* __restrict__ wide,
+    unsigned long long* __restrict__ ctr) {
   TableView tab, unused;
   lane_tables(ws, tab, unused);
   __shared__ uint4 tails[9][kBlock];
@@ -773,6 +852,12 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const bool live = t < cnt;
     HalfState h;
     ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
+    {  // the two roles of verify_prep_pair_kernel -> P1 = sign(c) A, P2 = sign(d) Q, final flags
+      const fe nAx = h.P1x, nAy = h.P1y, nQx = h.P2x, nQy = h.P2y;
+      finish_phase1_points(h, nAx, nAy, nQx, nQy, (h.pad & kPairPointOk) != 0);
+      if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+    }
+    const uint64_t fball = __ballot(live && (h.tops & kHalfFallback) != 0);
     ge_p2 mine, other;
     verify_phase2_pair_chain(mine, h, par, tab, wl);
 #pragma unroll
@@ -787,7 +872,11 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
 #pragma unroll
     for (int b = 0; b < 32; ++b) half |= (uint32_t)((ball >> (2 * b)) & 1u) << b;
     const uint32_t wsig = (tile + wave * 64) >> 1;  // first signature of this wave, a multiple of 32
+    uint32_t fhalf = 0;  // fallback flags of the even lanes, for verify_fallback_kernel
+#pragma unroll
+    for (int b = 0; b < 32; ++b) fhalf |= (uint32_t)((fball >> (2 * b)) & 1u) << b;
     if (lane == 0 && (wsig >> 6) < words) {
+      reinterpret_cast<uint32_t*>(fb_words)[wsig >> 5] = fhalf;
       reinterpret_cast<uint32_t*>(bitmap)[(base + wsig) >> 5] = half;
       if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popc(half));  // accepted (stl_get_stats)
     }
@@ -1298,7 +1387,16 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     }
     const bool fused = x.fused_prep != 0 && !pair_point && !dedup;
     mark(0);
-    if (fused && pre_k)
+    if (pair) {
+      // both halves of phase 1 in one launch, side by side (verify_prep_pair_kernel)
+      const uint32_t nbs = (cnt + kBlock - 1) / kBlock;
+      if (pre_k)
+        hipLaunchKernelGGL(verify_prep_pair_kernel<true>, dim3(nbs + gp.x), dim3(kBlock), 0, stream, sig, msg_or_k, pk,
+                           base, cnt, policy, pre, nbs);
+      else
+        hipLaunchKernelGGL(verify_prep_pair_kernel<false>, dim3(nbs + gp.x), dim3(kBlock), 0, stream, sig, msg_or_k,
+                           pk, base, cnt, policy, pre, nbs);
+    } else if (fused && pre_k)
       hipLaunchKernelGGL(verify_prep_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
                          pre, fb);
     else if (fused)
@@ -1309,7 +1407,7 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     else
       hipLaunchKernelGGL(verify_scalar_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     mark(1);
-    if (fused) {
+    if (fused || pair) {
       // phase 1 done
     } else if (pair_point) {
       hipLaunchKernelGGL(verify_point_pair_kernel, gp, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
@@ -1335,8 +1433,8 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     }
     mark(2);
     if (pair)
-      hipLaunchKernelGGL(verify_main_pair_kernel, gp, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
-                         counters);
+      hipLaunchKernelGGL(verify_main_pair_kernel, gp, dim3(kBlock), 0, stream, pre, base, cnt, policy, bitmap, fb,
+                         slots, wide, counters);
     else
       hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
                          counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr, qctr);
