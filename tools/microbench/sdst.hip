@@ -60,6 +60,24 @@ KERNEL(k_addco_s8, DECL32, M16(ADDCO_SD, P0, P1, P2, P3, P4, P5, P6, P7))
 #define LSHLADD_(c, s) LSHLADD(c)
 KERNEL(k_lshladd, DECL64, M16(LSHLADD_, 0, 0, 0, 0, 0, 0, 0, 0))
 
+
+// The same without clobber lists: the compiler sees no SGPR write, so it puts
+// no hazard s_nop between the mads (the clobbering forms above get one after
+// every mad, which a lone wave pays as a full issue slot).
+#define MAD_NC(c, sd) asm volatile("v_mad_u64_u32 %0, " sd ", %1, %2, %0" : "+v"(c) : "v"(x), "v"(b));
+#define Q0 "s[40:41]"
+#define Q1 "s[42:43]"
+#define Q2 "s[44:45]"
+#define Q3 "s[46:47]"
+#define Q4 "s[48:49]"
+#define Q5 "s[50:51]"
+#define Q6 "s[52:53]"
+#define Q7 "s[54:55]"
+KERNEL(k_madnc_one, DECL64, M16(MAD_NC, Q0, Q0, Q0, Q0, Q0, Q0, Q0, Q0))
+KERNEL(k_madnc_s2, DECL64, M16(MAD_NC, Q0, Q1, Q0, Q1, Q0, Q1, Q0, Q1))
+KERNEL(k_madnc_s4, DECL64, M16(MAD_NC, Q0, Q1, Q2, Q3, Q0, Q1, Q2, Q3))
+KERNEL(k_madnc_s8, DECL64, M16(MAD_NC, Q0, Q1, Q2, Q3, Q4, Q5, Q6, Q7))
+
 typedef void (*kfn)(uint64_t*, uint64_t*, uint32_t, uint32_t);
 
 static int run(kfn f, int cus, int w, double instrs_per_wave, double* out_simd_cycles, uint64_t* d, uint64_t* dc) {
@@ -89,7 +107,9 @@ int main() {
   struct { const char* name; kfn f; } ks[] = {
       {"mad64 sdst vcc", k_mad_vcc}, {"mad64 sdst one pair", k_mad_s1}, {"mad64 sdst 2 pairs", k_mad_s2},
       {"mad64 sdst 4 pairs", k_mad_s4}, {"mad64 sdst 8 pairs", k_mad_s8}, {"add_co vcc", k_addco_vcc},
-      {"add_co 8 pairs", k_addco_s8}, {"v_lshl_add_u64", k_lshladd}};
+      {"add_co 8 pairs", k_addco_s8}, {"v_lshl_add_u64", k_lshladd},
+      {"mad64 no-nop one pair", k_madnc_one}, {"mad64 no-nop 2 pairs", k_madnc_s2},
+      {"mad64 no-nop 4 pairs", k_madnc_s4}, {"mad64 no-nop 8 pairs", k_madnc_s8}};
   printf("%-22s %10s %10s %10s\n", "instruction", "W=1", "W=2", "W=4");
   for (auto& k : ks) {
     double c1, c2, c4;
