@@ -275,55 +275,6 @@ __device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
 #endif
 }
 
-// verify_point_kernel for small chunks (the pair chunks of
-// verify_main_pair_kernel): lanes 2j and 2j+1 decode signature j's A and R,
-// one square-root chain each, swap the results and finish together; lane 0
-// writes the state, a wave's even ballot bits are a 32-bit half of a
-// fallback word.  At most one wave per SIMD runs it (pair_max), so it takes
-// the registers of 2 waves/SIMD and does not spill.
-__global__ __launch_bounds__(kBlock, 2) void verify_point_pair_kernel(
-    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk, uint32_t base, uint32_t cnt, uint32_t policy,
-    uint4* __restrict__ pre, uint64_t* __restrict__ fb_words) {
-  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t t = g >> 1;
-  const int par = (int)(g & 1u);
-  const bool live = t < cnt;
-  const uint32_t tt = live ? t : cnt - 1;
-  const size_t j = (size_t)base + tt;
-  uint32_t R[8], S[8], A[8];
-  ld8(R, sig + 64 * j);
-  ld8(S, sig + 64 * j + 32);
-  ld8(A, pk + 32 * j);
-  uint4* q = pre + (size_t)tt * 14;
-  HalfState h;
-  uint32_t* w = reinterpret_cast<uint32_t*>(&h);
-  const uint4 q2 = q[kHalfTopsWord / 4];
-  w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
-  fe mx, my, ox, oy;
-  const bool mok = phase1_decode_lane(mx, my, R, A, par);
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    ox.v[i] = pair_swap(mx.v[i]);
-    oy.v[i] = pair_swap(my.v[i]);
-  }
-  const bool ook = pair_swap((uint32_t)mok) != 0;
-  if (par == 0)
-    phase1_points_finish_pair(h, R, S, A, core_policy(policy), mx, my, mok, ox, oy, ook);
-  else
-    phase1_points_finish_pair(h, R, S, A, core_policy(policy), ox, oy, ook, mx, my, mok);
-  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
-  if (live && par == 0) {
-    st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
-#pragma unroll
-    for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
-  }
-  const uint64_t ball = __ballot(live && (h.tops & kHalfFallback) != 0);
-  uint32_t half = 0;
-#pragma unroll
-  for (int b = 0; b < 32; ++b) half |= (uint32_t)((ball >> (2 * b)) & 1u) << b;
-  const uint32_t wsig = (g & ~63u) >> 1;  // first signature of this wave, a multiple of 32
-  if ((threadIdx.x & 63u) == 0 && (wsig >> 6) < ((cnt + 63) >> 6)) reinterpret_cast<uint32_t*>(fb_words)[wsig >> 5] = half;
-}
 
 // Phase 1 of the lane-pair path (chunks that run verify_main_pair_kernel) as
 // ONE launch whose workgroups take one of two roles, so the scalar half
@@ -388,7 +339,7 @@ __global__ __launch_bounds__(kBlock, 2) void verify_prep_pair_kernel(
     uint32_t S[8];
     ld8(S, sig + 64 * j + 32);
     const uint32_t pol = core_policy(policy);
-    const bool ok = verify_prechecks(R, S, A, pol) && composite_s_ok(S, pol) && r_is_canonical(R) && mok && ook;
+    const bool ok = phase1_points_ok(R, S, A, pol, mok, ook);
     HalfState h;
     h.P1x = mx;
     h.P1y = my;
@@ -401,6 +352,32 @@ __global__ __launch_bounds__(kBlock, 2) void verify_prep_pair_kernel(
 #pragma unroll
     for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
   }
+}
+
+// After verify_prep_pair_kernel, for chunks whose point decodings run on lane
+// pairs but whose main kernel runs one lane per signature (between a quarter
+// and a half of the resident lanes): the two roles' words -> the finished
+// HalfState the one-lane main kernel reads, and the fallback words, one lane
+// per signature.
+__global__ __launch_bounds__(kBlock) void verify_finish_pair_kernel(uint32_t cnt, uint32_t policy,
+                                                                    uint4* __restrict__ pre,
+                                                                    uint64_t* __restrict__ fb_words) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = t < cnt;
+  uint4* q = pre + (size_t)(live ? t : cnt - 1) * 14;
+  HalfState h;
+  ld_state_words<14>(h, q);
+  const fe nAx = h.P1x, nAy = h.P1y, nQx = h.P2x, nQy = h.P2y;
+  finish_phase1_points(h, nAx, nAy, nQx, nQy, (h.pad & kPairPointOk) != 0);
+  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  if (live) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&h);
+    st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
+#pragma unroll
+    for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+  }
+  const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
+  if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
 
 // ---- per-batch key dedup (STL_DEDUP_KEYS) ----
@@ -1349,15 +1326,16 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     const uint32_t units = (cnt + 63) / 64;
     const uint32_t wgs = (units + kBlock / 64 - 1) / (kBlock / 64);
     const dim3 g2(wgs < grid ? wgs : grid);
-    // Small chunks: two lanes per signature in the point and main kernels
-    // (verify_point_pair_kernel, verify_main_pair_kernel); the bits are the
+    // Small chunks: two lanes per signature in the point decodings and the main
+    // kernel (verify_prep_pair_kernel, verify_main_pair_kernel); the bits are the
     // same.  It also takes precedence over key dedup: a chunk this small is
     // latency-bound, and measured 0.46-0.52 ms on pairs against 0.68-0.75 ms
     // deduplicated (1,000 signers).
     const bool pair = (policy & kModeOneLane) == 0 && cnt <= pair_max && 2ull * cnt <= (uint64_t)grid * kBlock;
-    // The point kernel's pairs split its two square roots without duplicating
-    // work, so they pay up to twice that size (two pair waves per SIMD; no
-    // workspace), ahead of the one-lane main kernel.
+    // The point decodings' pairs split the two square roots without
+    // duplicating work, so they pay up to twice that size (two pair waves per
+    // SIMD; no workspace), ahead of the one-lane main kernel
+    // (verify_finish_pair_kernel in between).
 #ifdef STL_POINT_PAIR_ALL
     const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup);
 #else
@@ -1387,8 +1365,11 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     }
     const bool fused = x.fused_prep != 0 && !pair_point && !dedup;
     mark(0);
-    if (pair) {
-      // both halves of phase 1 in one launch, side by side (verify_prep_pair_kernel)
+    // pair_point implies !dedup or pair (pair chunks ignore STL_DEDUP_KEYS)
+    if (pair_point) {
+      // both halves of phase 1 in one launch, side by side (verify_prep_pair_kernel);
+      // the main pair kernel finishes the state itself, the one-lane main
+      // kernel gets it from verify_finish_pair_kernel
       const uint32_t nbs = (cnt + kBlock - 1) / kBlock;
       if (pre_k)
         hipLaunchKernelGGL(verify_prep_pair_kernel<true>, dim3(nbs + gp.x), dim3(kBlock), 0, stream, sig, msg_or_k, pk,
@@ -1407,10 +1388,11 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     else
       hipLaunchKernelGGL(verify_scalar_kernel<false>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, pre);
     mark(1);
-    if (fused || pair) {
+    if (pair_point) {
+      if (!pair)
+        hipLaunchKernelGGL(verify_finish_pair_kernel, g1, dim3(kBlock), 0, stream, cnt, policy, pre, fb);
+    } else if (fused) {
       // phase 1 done
-    } else if (pair_point) {
-      hipLaunchKernelGGL(verify_point_pair_kernel, gp, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     } else if (dedup) {
       uint32_t nslots = 64;
       while (nslots < 2 * cnt) nslots <<= 1;  // <= kDedupSlots

@@ -448,7 +448,8 @@ STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32
 
 // Small batches: verify_phase1_points on a lane pair, one decoding per lane
 // (`par` 0 decodes A, 1 decodes R, into -A / -Q); the pair swaps the results
-// and both lanes finish with phase1_points_finish_pair.
+// (verify_prep_pair_kernel); phase1_points_ok gives the pair's flag and
+// finish_phase1_points the signed P1 / P2.
 STL_HD bool phase1_decode_lane(fe& nx, fe& ny, const uint32_t R[8], const uint32_t A[8], int par) {
   uint32_t P[8];
 #pragma unroll
@@ -460,12 +461,11 @@ STL_HD bool phase1_decode_lane(fe& nx, fe& ny, const uint32_t R[8], const uint32
   return ok;
 }
 
-STL_HD void phase1_points_finish_pair(HalfState& o, const uint32_t R[8], const uint32_t S[8], const uint32_t A[8],
-                                      uint32_t policy, const fe& nAx, const fe& nAy, bool okA, const fe& nQx,
-                                      const fe& nQy, bool okR) {
-  bool ok = verify_prechecks(R, S, A, policy);
-  ok = ok && composite_s_ok(S, policy) && r_is_canonical(R) && okA && okR;
-  finish_phase1_points(o, nAx, nAy, nQx, nQy, ok);
+// The point role's flag (verify_prep_pair_kernel): the pre-checks of the
+// policy, stellard's S < L, a canonical R and both decodings.
+STL_HD bool phase1_points_ok(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], uint32_t policy, bool okA,
+                             bool okR) {
+  return verify_prechecks(R, S, A, policy) && composite_s_ok(S, policy) && r_is_canonical(R) && okA && okR;
 }
 
 // Phase 1, point half, with -A decoded once per distinct key of the batch

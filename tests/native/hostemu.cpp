@@ -153,7 +153,7 @@ uint64_t hostemu_verify_batch_split(const uint8_t* sig, const uint8_t* msg, cons
   return g_bound_viol.load();
 }
 
-// The small-batch pair path (verify_point_pair_kernel +
+// The small-batch pair path (verify_prep_pair_kernel +
 // verify_main_pair_kernel): each signature's two decodings, its two
 // chains (verify_phase2_pair_chain, parity 0 and 1, each on its own split
 // table with the kernel's LDS tail stride) and the pair's cancellation check.
@@ -180,9 +180,9 @@ uint64_t hostemu_verify_batch_pair(const uint8_t* sig, const uint8_t* msg, const
     stl::sc_reduce64(k, h);
     stl::HalfState hs;
     stl::verify_phase1_scalars(hs, S, k);
-    stl::fe ax, ay, qx, qy;  // the pair's two decodings (verify_point_pair_kernel)
+    stl::fe ax, ay, qx, qy;  // the pair's two decodings (the point role of verify_prep_pair_kernel)
     const bool okA = stl::phase1_decode_lane(ax, ay, R, A, 0), okR = stl::phase1_decode_lane(qx, qy, R, A, 1);
-    stl::phase1_points_finish_pair(hs, R, S, A, policy, ax, ay, okA, qx, qy, okR);
+    stl::finish_phase1_points(hs, ax, ay, qx, qy, stl::phase1_points_ok(R, S, A, policy, okA, okR));
     bool ok;
     if (hs.tops & stl::kHalfFallback) {
       ok = stl::verify_full_with_k(R, S, A, k, policy, tf, btab);

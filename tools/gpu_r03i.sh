@@ -3,7 +3,7 @@
 # previous build (scalar kernel, then the point-pair kernel): GPU suite on the
 # new build, then phase_small ABAB and single-call latency of both.
 set -o pipefail
-OUT=r03i
+OUT=${OUT:-r03i}
 mkdir -p gpurun_out/$OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$OUT/pytest_gpu.log 2>&1
 rc=$?; echo "gpu tests rc=$rc"; tail -2 gpurun_out/$OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
