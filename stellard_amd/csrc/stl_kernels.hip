@@ -688,6 +688,10 @@ struct WideGlobal {
 #else
 #define STL_MAIN_ATTR
 #endif
+// JOINT (chunks without key dedup): one joint radix-4 table of a*P1 + b*P2
+// per lane (verify_phase2_joint); otherwise two radix-16 tables, the A-table
+// possibly the key's shared one (verify_phase2_half).
+template <bool JOINT>
 __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
     uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
@@ -728,7 +732,11 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const bool live = t < cnt;
     HalfState h;
     ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
-    const bool ok = verify_phase2_half(h, tab1, tab2, wl, keytabs, widetabs) && live;
+    bool ok;
+    if (JOINT)
+      ok = verify_phase2_joint(h, tab1, wl) && live;
+    else
+      ok = verify_phase2_half(h, tab1, tab2, wl, keytabs, widetabs) && live;
     const uint64_t word = __ballot(ok);
     if (lane == 0) {
       bitmap[(base + wbase) >> 6] = word;
@@ -1261,7 +1269,7 @@ __global__ __launch_bounds__(kBlock, 2) void sign_kernel(const uint8_t* __restri
 }
 
 // ---- host-side launchers (called from stl_api.cpp) ----
-const void* kernel_verify_msg32() { return reinterpret_cast<const void*>(&verify_main_kernel); }
+const void* kernel_verify_msg32() { return reinterpret_cast<const void*>(&verify_main_kernel<false>); }
 
 // Wide base tables: one thread per row (stl_verify_core.h wide_entry).
 __global__ __launch_bounds__(kBlock) void wide_table_kernel(uint32_t* __restrict__ out) {
@@ -1417,8 +1425,13 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     if (pair)
       hipLaunchKernelGGL(verify_main_pair_kernel, gp, dim3(kBlock), 0, stream, pre, base, cnt, policy, bitmap, fb,
                          slots, wide, counters);
+#ifndef STL_NO_JOINT
+    else if (!dedup)
+      hipLaunchKernelGGL(verify_main_kernel<true>, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
+                         counters, nullptr, nullptr, qctr);
+#endif
     else
-      hipLaunchKernelGGL(verify_main_kernel, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
+      hipLaunchKernelGGL(verify_main_kernel<false>, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
                          counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr, qctr);
     mark(3);
     if (pre_k)

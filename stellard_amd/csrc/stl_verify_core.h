@@ -191,8 +191,14 @@ STL_HD void build_cached_table(const TableView& tab, const ge_p3& P) {
   ge_p1p1_to_p3(p3, t);
   ge_p3_to_cached(c, p3);
   tab.store(2, c);
+#ifdef STL_EXP_TABLE_ENTRIES
+#warning "STL_EXP_TABLE_ENTRIES is a timing experiment: verification results are wrong"
+  constexpr int kLast = STL_EXP_TABLE_ENTRIES;
+#else
+  constexpr int kLast = 8;
+#endif
 #pragma unroll 1
-  for (int e = 3; e <= 8; ++e) {
+  for (int e = 3; e <= kLast; ++e) {
     ge_madd(t, p3, n1);
     ge_p1p1_to_p3(p3, t);
     ge_p3_to_cached(c, p3);
@@ -690,8 +696,13 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     // a load under `if (cadd)` made the compiler merge its registers at the
     // end of the branch, i.e. wait for the load there -- before the doublings
     // it is meant to overlap.
+#if defined(STL_EXP_TABLE_ENTRIES)
+    t1.load(cadd ? min(dc < 0 ? -dc : dc, STL_EXP_TABLE_ENTRIES) : 0, ca);
+    tab2.load(min(dq < 0 ? -dq : dq, STL_EXP_TABLE_ENTRIES), cq);
+#else
     t1.load(cadd ? (dc < 0 ? -dc : dc) : 0, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
+#endif
 #endif
     if (bpos) wide.prefetch(de0, de1);
     if (i != npos - 1) dbl4(acc, acc2);
@@ -717,6 +728,219 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     }
   }
   // identity: X == 0 and Y == Z
+  fe ymz;
+  fe_sub(ymz, acc2.Y, acc2.Z);
+  const bool id = fe_iszero(acc2.X) && fe_iszero(ymz);
+  return (p.tops & kHalfOk) != 0 && (p.tops & kHalfFallback) == 0 && id;
+}
+
+// ---- joint radix-4 table (round 3): one per-lane table for both points ----
+// c and d in signed radix 16 (digits D in [-8, 7]) are read as signed radix 4:
+// D = 4q + r with r = ((D + 2) mod 4) - 2 in [-2, 1] and q in [-2, 2], so a
+// nibble position becomes two sub-positions, each two doublings and ONE add
+// of a*P1 + b*P2 with (a, b) in [-2, 2]^2 -- the same 4 doublings and 2 adds
+// per nibble as two radix-16 tables, but the table holds 12 entries (the
+// pairs up to sign) instead of 2 x 8, built with 36 products fewer, and the
+// per-lane heads shrink from 2 KiB to 1.5 KiB.  Index of (a, b) up to sign:
+//   (0, 1), (0, 2)                      -> 1, 2
+//   (1, b), b = -2..2 / (2, b)          -> 3..7 / 8..12
+// entry 0 is the identity (a = b = 0).
+constexpr int kJointEntries = 12;
+
+STL_HD int joint_index(int a, int b, bool& neg) {
+  neg = a < 0 || (a == 0 && b < 0);
+  if (neg) {
+    a = -a;
+    b = -b;
+  }
+  return a == 0 ? b : 3 + (a - 1) * 5 + (b + 2);
+}
+
+// -(cached point) with every limb normalised (T2d [1], so a lookup may negate
+// it again with fe_neg_nc<2>)
+STL_HD void ge_cached_neg_norm(ge_cached& c) {
+  const fe a = c.YpX;
+  c.YpX = c.YmX;
+  c.YmX = a;
+  fe_neg(c.T2d, c.T2d);
+}
+
+// p3 -> cached, stored at entry e
+STL_HD void joint_store(const TableView& tab, int e, const ge_p3& P) {
+  ge_cached c;
+  ge_p3_to_cached(c, P);
+  tab.store(e, c);
+}
+
+// 2P from a p3 point (a projective doubling), -> p3
+STL_HD void ge_p3_dbl_p3(ge_p3& r, const ge_p3& P) {
+  ge_p2 p2;
+  ge_p1p1 t;
+  ge_p3_to_p2(p2, P);
+  ge_p2_dbl(t, p2);
+  ge_p1p1_to_p3(r, t);
+}
+
+// The 12 entries a*P1 + b*P2 from the affine P1 = (x1, y1), P2 = (x2, y2),
+// ordered so that at most three points are live at a time: 72 M + 14 S
+// against 108 M + 6 S for two 8-entry tables.
+STL_HD void build_joint_table(const TableView& tab, const fe& x1, const fe& y1, const fe& x2, const fe& y2) {
+  ge_cached c0;
+  ge_cached_0(c0);
+  tab.store(0, c0);
+  ge_p1p1 t;
+  ge_niels n2;
+  {
+    ge_p3 P2;
+    affine_to_p3(P2, x2, y2);
+    ge_cached c;
+    ge_p3_to_cached(c, P2);  // Z = 1: the cached form is P2's Niels form
+    tab.store(1, c);         // (0, 1)
+    n2.ypx = c.YpX;
+    n2.ymx = c.YmX;
+    n2.xy2d = c.T2d;
+  }
+  {
+    ge_p3 P1;
+    affine_to_p3(P1, x1, y1);
+    joint_store(tab, 5, P1);  // (1, 0)
+    ge_p3 S;
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {  // P1 + P2, then P1 - P2, and their doubles
+      ge_niels n = n2;
+      ge_niels_cneg(n, s == 1);
+      ge_madd(t, P1, n);
+      ge_p1p1_to_p3(S, t);
+      joint_store(tab, s == 0 ? 6 : 4, S);  // (1, 1) / (1, -1)
+      ge_p3_dbl_p3(S, S);
+      joint_store(tab, s == 0 ? 12 : 8, S);  // (2, 2) / (2, -2)
+    }
+    ge_affine_dbl(t, P1);
+    ge_p1p1_to_p3(P1, t);  // P1 <- 2 P1
+    joint_store(tab, 10, P1);  // (2, 0)
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {  // 2 P1 + P2, 2 P1 - P2
+      ge_niels n = n2;
+      ge_niels_cneg(n, s == 1);
+      ge_madd(t, P1, n);
+      ge_p1p1_to_p3(S, t);
+      joint_store(tab, s == 0 ? 11 : 9, S);  // (2, 1) / (2, -1)
+    }
+  }
+  {
+    ge_niels n1;  // P1's Niels form = its stored cached entry (Z = 1)
+    {
+      ge_cached c;
+      tab.load(5, c);
+      n1.ypx = c.YpX;
+      n1.ymx = c.YmX;
+      n1.xy2d = c.T2d;
+    }
+    ge_p3 Q;
+    affine_to_p3(Q, x2, y2);
+    ge_affine_dbl(t, Q);
+    ge_p1p1_to_p3(Q, t);  // 2 P2
+    joint_store(tab, 2, Q);  // (0, 2)
+    ge_p3 S;
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {  // 2 P2 + P1 = (1, 2); 2 P2 - P1 = -(1, -2)
+      ge_niels n = n1;
+      ge_niels_cneg(n, s == 1);
+      ge_madd(t, Q, n);
+      ge_p1p1_to_p3(S, t);
+      ge_cached c;
+      ge_p3_to_cached(c, S);
+      if (s == 1) ge_cached_neg_norm(c);
+      tab.store(s == 0 ? 7 : 3, c);
+    }
+  }
+}
+
+// Phase 2 with the joint table: [e]B + [c](-A) + [d](-Q) == O as in
+// verify_phase2_half (same digits, same wide-table madds at every fourth
+// nibble position, same identity test); one table, one add per sub-position.
+template <typename Wide>
+STL_HD bool verify_phase2_joint(const HalfState& p, const TableView& tab, Wide& wide) {
+  build_joint_table(tab, p.P1x, p.P1y, p.P2x, p.P2y);
+  const int npos = half_positions((int)(p.tops & 0xffu));
+  uint32_t cd[5], dd[5], ed[8];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    cd[i] = p.cdig[i];
+    dd[i] = p.ddig[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ed[i] = p.edig[i];
+  ge_p3 acc;
+  ge_p2 acc2;
+  ge_p1p1 t;
+  ge_p3_0(acc);
+  ge_p2_0(acc2);
+  uint32_t wc = 0, wd = 0, we0 = 0, we1 = 0;
+#pragma unroll 1
+  for (int i = kHalfDigits - 1; i >= 0; --i) {
+    if ((i & 7) == 7) {
+      wc = cd[4];
+      wd = dd[4];
+#pragma unroll
+      for (int m = 4; m > 0; --m) {
+        cd[m] = cd[m - 1];
+        dd[m] = dd[m - 1];
+      }
+    }
+    if ((i & 7) == 4 && i < 32) {
+      we0 = ed[3];
+      we1 = ed[7];
+#pragma unroll
+      for (int m = 3; m > 0; --m) {
+        ed[m] = ed[m - 1];
+        ed[4 + m] = ed[4 + m - 1];
+      }
+    }
+    const int dc = (int32_t)wc >> 28;
+    const int dq = (int32_t)wd >> 28;
+    wc <<= 4;
+    wd <<= 4;
+    const bool bpos = (i & 3) == 0 && i < 32;  // wave-uniform
+    int de0 = 0, de1 = 0;
+    if (bpos) {
+      de0 = (i & 4) ? (int32_t)we0 >> 16 : (int32_t)(we0 << 16) >> 16;
+      de1 = (i & 4) ? (int32_t)we1 >> 16 : (int32_t)(we1 << 16) >> 16;
+    }
+    if (i >= npos) continue;  // wave-uniform
+    const int cr = ((dc + 2) & 3) - 2, dr = ((dq + 2) & 3) - 2;
+    bool n0, n1;
+    const int e0 = joint_index((dc - cr) >> 2, (dq - dr) >> 2, n0);
+    const int e1 = joint_index(cr, dr, n1);
+    ge_cached c0, c1;
+    tab.load(e0, c0);  // both loads ahead of the doublings, as in verify_phase2_half
+    tab.load(e1, c1);
+    if (bpos) wide.prefetch(de0, de1);
+    if (i != npos - 1) {
+      ge_p2_dbl<true>(t, acc2);
+      ge_p1p1_to_p2(acc2, t);
+      ge_p2_dbl(t, acc2);
+      ge_p1p1_to_p3(acc, t);
+    }
+    ge_cached_cneg(c0, n0);
+    ge_add_cached(t, acc, c0);
+    ge_p1p1_to_p2(acc2, t);
+    ge_p2_dbl<true>(t, acc2);
+    ge_p1p1_to_p2(acc2, t);
+    ge_p2_dbl(t, acc2);
+    ge_p1p1_to_p3(acc, t);
+    ge_cached_cneg(c1, n1);
+    ge_add_cached(t, acc, c1);
+    if (!bpos) {
+      ge_p1p1_to_p2(acc2, t);
+    } else {
+      ge_p1p1_to_p3(acc, t);
+      wide.madd(t, acc, 0);
+      ge_p1p1_to_p3(acc, t);
+      wide.madd(t, acc, 1);
+      ge_p1p1_to_p2(acc2, t);
+    }
+  }
   fe ymz;
   fe_sub(ymz, acc2.Y, acc2.Z);
   const bool id = fe_iszero(acc2.X) && fe_iszero(ymz);

@@ -153,6 +153,42 @@ uint64_t hostemu_verify_batch_split(const uint8_t* sig, const uint8_t* msg, cons
   return g_bound_viol.load();
 }
 
+// The main kernel's default path (verify_main_kernel<JOINT = true>): one
+// joint radix-4 table of a*P1 + b*P2 per lane in the split layout (heads of
+// entries 1-12, tails at stride `tstride`), verify_phase2_joint.
+uint64_t hostemu_verify_batch_joint(const uint8_t* sig, const uint8_t* msg, const uint8_t* pk, size_t n,
+                                    uint8_t* bitmap, uint32_t policy, int tstride) {
+  std::vector<uint4> heads(2 * 8 * 8), tails((size_t)18 * tstride), id(9);
+  stl::ge_cached idc;
+  stl::ge_cached_0(idc);
+  stl::TableView::contiguous(id.data()).store(0, idc);
+  const stl::TableView tj = stl::TableView::split(heads.data(), tails.data(), id.data(), tstride);
+  std::vector<uint4> full(81);
+  const stl::TableView tf = stl::TableView::contiguous(full.data());
+  const uint32_t* btab = &stl::kBaseNielsHost[0][0][0];
+  std::memset(bitmap, 0, (n + 7) / 8);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t R[8], S[8], A[8], M[8], h[16], k[8];
+    load8(R, sig + 64 * i);
+    load8(S, sig + 64 * i + 32);
+    load8(A, pk + 32 * i);
+    load8(M, msg + 32 * i);
+    stl::sha512_hram32(h, R, A, M);
+    stl::sc_reduce64(k, h);
+    stl::HalfState hs;
+    stl::verify_phase1_half(hs, R, S, A, k, policy);
+    bool ok;
+    if (hs.tops & stl::kHalfFallback) {
+      ok = stl::verify_full_with_k(R, S, A, k, policy, tf, btab);
+    } else {
+      stl::WideHost wide{wide_tables(), {0, 0}};
+      ok = stl::verify_phase2_joint(hs, tj, wide);
+    }
+    if (ok) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  return g_bound_viol.load();
+}
+
 // The small-batch pair path (verify_prep_pair_kernel +
 // verify_main_pair_kernel): each signature's two decodings, its two
 // chains (verify_phase2_pair_chain, parity 0 and 1, each on its own split

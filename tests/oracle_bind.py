@@ -273,6 +273,8 @@ def load_hostemu():
     lib.hostemu_verify_batch_mode.argtypes = [V, V, V, ctypes.c_size_t, V, ctypes.c_uint32, ctypes.c_int, V]
     lib.hostemu_verify_batch_split.restype = ctypes.c_uint64
     lib.hostemu_verify_batch_split.argtypes = [V, V, V, ctypes.c_size_t, V, ctypes.c_uint32, ctypes.c_int]
+    lib.hostemu_verify_batch_joint.restype = ctypes.c_uint64
+    lib.hostemu_verify_batch_joint.argtypes = [V, V, V, ctypes.c_size_t, V, ctypes.c_uint32, ctypes.c_int]
     lib.hostemu_verify_batch_pair.restype = ctypes.c_uint64
     lib.hostemu_verify_batch_pair.argtypes = [V, V, V, ctypes.c_size_t, V, ctypes.c_uint32]
     lib.hostemu_identity_head.argtypes = [V]

@@ -186,6 +186,50 @@ def test_split_table_layout_vs_golden(emu, golden, policy, key, tstride):
     assert np.array_equal(got, golden[key].astype(bool))
 
 
+@pytest.mark.parametrize("tstride", [1, 256])
+@pytest.mark.parametrize("policy,key", [(0, "expected_sodium_1_0_18"), (1, "expected_stellard_1_0_0_unpinned")])
+def test_joint_table_vs_golden(emu, golden, policy, key, tstride):
+    """The main kernel's default path: one joint radix-4 table of a*P1 + b*P2
+    per lane (build_joint_table, verify_phase2_joint), split layout with the
+    LDS tail stride, gives the golden bits with zero limb-bound violations
+    (the table build adds, doubles and negates entries the old tables never
+    held)."""
+    sig, msg, pk = golden["sig"], golden["msg"], golden["pk"]
+    n = sig.shape[0]
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    B = lambda a: np.ascontiguousarray(a).ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    viol = emu.hostemu_verify_batch_joint(B(sig), B(msg), B(pk), n, B(bm), policy, tstride)
+    assert viol == 0
+    got = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    exp = golden[key].astype(bool)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, [(int(i), str(golden["class_names"][golden["cls"][i]])) for i in bad[:10]]
+
+
+def test_joint_table_vs_oracle_random(emu, oracle):
+    """Random valid and mutated signatures through the joint path against the
+    oracle (every digit pair of the joint table gets exercised)."""
+    rng = np.random.default_rng(0x7A61)
+    n = 3000
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pk = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    for i in range(n):
+        p, sk = oracle.keypair(seeds[i].tobytes())
+        pk[i] = np.frombuffer(p, np.uint8)
+        sig[i] = np.frombuffer(oracle.sign(msgs[i].tobytes(), sk), np.uint8)
+    flip = rng.choice(n, n // 5, replace=False)
+    sig[flip, rng.integers(0, 64, flip.size)] ^= 1 << rng.integers(0, 8, flip.size).astype(np.uint8)
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    B = lambda a: np.ascontiguousarray(a).ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    assert emu.hostemu_verify_batch_joint(B(sig), B(msgs), B(pk), n, B(bm), 0, 256) == 0
+    got = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    exp = oracle.verify_batch(sig, msgs, pk)
+    assert np.array_equal(got, exp)
+    assert 0 < int(got.sum()) < n
+
+
 @pytest.mark.parametrize("policy,key", [(0, "expected_sodium_1_0_18"), (1, "expected_stellard_1_0_0_unpinned")])
 def test_pair_chains_vs_golden(emu, golden, policy, key):
     """The small-batch pair path (verify_phase2_pair_chain on two lanes,

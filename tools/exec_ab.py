@@ -58,6 +58,8 @@ def main():
         V.verify_batch_device(sig, msgs, pk, out_words=words, stream=s)
         torch.cuda.synchronize()
         bits = V.words_to_bool(words, n)
+        if os.environ.get("STL_AB_TIMING_ONLY"):  # timing-only builds (STL_EXP_*): results are wrong by design
+            continue
         if ref is None:
             ref = bits
             assert int(bits.sum()) == n - n // 100, "parity failure"
