@@ -730,13 +730,15 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
     const uint32_t wbase = unit * 64;
     const uint32_t t = wbase + lane;
     const bool live = t < cnt;
-    HalfState h;
-    ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
+    const uint4* st = pre + (size_t)(live ? t : cnt - 1) * 14;
     bool ok;
-    if (JOINT)
-      ok = verify_phase2_joint(h, tab1, wl) && live;
-    else
+    if (JOINT) {
+      ok = verify_phase2_joint(st, tab1, wl) && live;
+    } else {
+      HalfState h;
+      ld_state_words<14>(h, st);
       ok = verify_phase2_half(h, tab1, tab2, wl, keytabs, widetabs) && live;
+    }
     const uint64_t word = __ballot(ok);
     if (lane == 0) {
       bitmap[(base + wbase) >> 6] = word;

@@ -781,34 +781,54 @@ STL_HD void ge_p3_dbl_p3(ge_p3& r, const ge_p3& P) {
   ge_p1p1_to_p3(r, t);
 }
 
-// The 12 entries a*P1 + b*P2 from the affine P1 = (x1, y1), P2 = (x2, y2),
-// ordered so that at most three points are live at a time: 72 M + 14 S
-// against 108 M + 6 S for two 8-entry tables.
-STL_HD void build_joint_table(const TableView& tab, const fe& x1, const fe& y1, const fe& x2, const fe& y2) {
-  ge_cached c0;
-  ge_cached_0(c0);
-  tab.store(0, c0);
+// Affine point i (0: P1, 1: P2) of a HalfState in memory (words 20-55).
+STL_HD void state_point(ge_p3& P, const uint4* state, int i) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(state) + 20 + 18 * i;
+  fe x, y;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    x.v[k] = w[k];
+    y.v[k] = w[9 + k];
+  }
+  affine_to_p3(P, x, y);
+}
+
+// Niels form of a stored Z = 1 entry (P1 at 5, P2 at 1), sign applied.
+STL_HD void joint_niels(ge_niels& n, const TableView& tab, int e, bool neg) {
+  ge_cached c;
+  tab.load(e, c);
+  n.ypx = c.YpX;
+  n.ymx = c.YmX;
+  n.xy2d = c.T2d;
+  ge_niels_cneg(n, neg);
+}
+
+// The 12 entries a*P1 + b*P2 from the affine P1, P2 of the lane's HalfState
+// in memory: 72 M + 14 S against 108 M + 6 S for two 8-entry tables.  Points
+// are re-read from the state and Niels forms from the entries already stored
+// (L1 / L2 hits) rather than held, so at most two points and one Niels form
+// are live next to the products' registers.
+STL_HD void build_joint_table(const TableView& tab, const uint4* state) {
   ge_p1p1 t;
-  ge_niels n2;
   {
-    ge_p3 P2;
-    affine_to_p3(P2, x2, y2);
     ge_cached c;
-    ge_p3_to_cached(c, P2);  // Z = 1: the cached form is P2's Niels form
-    tab.store(1, c);         // (0, 1)
-    n2.ypx = c.YpX;
-    n2.ymx = c.YmX;
-    n2.xy2d = c.T2d;
+    ge_cached_0(c);
+    tab.store(0, c);
+    ge_p3 P2;
+    state_point(P2, state, 1);
+    joint_store(tab, 1, P2);  // (0, 1); Z = 1, so its cached form is its Niels form
+    ge_affine_dbl(t, P2);
+    ge_p1p1_to_p3(P2, t);
+    joint_store(tab, 2, P2);  // (0, 2)
   }
   {
-    ge_p3 P1;
-    affine_to_p3(P1, x1, y1);
+    ge_p3 P1, S;
+    state_point(P1, state, 0);
     joint_store(tab, 5, P1);  // (1, 0)
-    ge_p3 S;
 #pragma unroll 1
     for (int s = 0; s < 2; ++s) {  // P1 + P2, then P1 - P2, and their doubles
-      ge_niels n = n2;
-      ge_niels_cneg(n, s == 1);
+      ge_niels n;
+      joint_niels(n, tab, 1, s == 1);
       ge_madd(t, P1, n);
       ge_p1p1_to_p3(S, t);
       joint_store(tab, s == 0 ? 6 : 4, S);  // (1, 1) / (1, -1)
@@ -820,32 +840,22 @@ STL_HD void build_joint_table(const TableView& tab, const fe& x1, const fe& y1, 
     joint_store(tab, 10, P1);  // (2, 0)
 #pragma unroll 1
     for (int s = 0; s < 2; ++s) {  // 2 P1 + P2, 2 P1 - P2
-      ge_niels n = n2;
-      ge_niels_cneg(n, s == 1);
+      ge_niels n;
+      joint_niels(n, tab, 1, s == 1);
       ge_madd(t, P1, n);
       ge_p1p1_to_p3(S, t);
       joint_store(tab, s == 0 ? 11 : 9, S);  // (2, 1) / (2, -1)
     }
   }
   {
-    ge_niels n1;  // P1's Niels form = its stored cached entry (Z = 1)
-    {
-      ge_cached c;
-      tab.load(5, c);
-      n1.ypx = c.YpX;
-      n1.ymx = c.YmX;
-      n1.xy2d = c.T2d;
-    }
-    ge_p3 Q;
-    affine_to_p3(Q, x2, y2);
+    ge_p3 Q, S;
+    state_point(Q, state, 1);
     ge_affine_dbl(t, Q);
-    ge_p1p1_to_p3(Q, t);  // 2 P2
-    joint_store(tab, 2, Q);  // (0, 2)
-    ge_p3 S;
+    ge_p1p1_to_p3(Q, t);  // 2 P2 (recomputed: cheaper than holding it)
 #pragma unroll 1
     for (int s = 0; s < 2; ++s) {  // 2 P2 + P1 = (1, 2); 2 P2 - P1 = -(1, -2)
-      ge_niels n = n1;
-      ge_niels_cneg(n, s == 1);
+      ge_niels n;
+      joint_niels(n, tab, 5, s == 1);
       ge_madd(t, Q, n);
       ge_p1p1_to_p3(S, t);
       ge_cached c;
@@ -859,9 +869,22 @@ STL_HD void build_joint_table(const TableView& tab, const fe& x1, const fe& y1, 
 // Phase 2 with the joint table: [e]B + [c](-A) + [d](-Q) == O as in
 // verify_phase2_half (same digits, same wide-table madds at every fourth
 // nibble position, same identity test); one table, one add per sub-position.
+// `state` is the lane's HalfState in memory (14 quads): the points are read
+// for the table build, the digits and flags only after it, so they are not
+// held in registers across the build.
 template <typename Wide>
-STL_HD bool verify_phase2_joint(const HalfState& p, const TableView& tab, Wide& wide) {
-  build_joint_table(tab, p.P1x, p.P1y, p.P2x, p.P2y);
+STL_HD bool verify_phase2_joint(const uint4* state, const TableView& tab, Wide& wide) {
+  build_joint_table(tab, state);
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" ::: "memory");  // the digit loads stay after the build
+#endif
+  HalfState p;
+  {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&p);
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(state);
+#pragma unroll
+    for (int i = 0; i < 20; ++i) w[i] = s[i];
+  }
   const int npos = half_positions((int)(p.tops & 0xffu));
   uint32_t cd[5], dd[5], ed[8];
 #pragma unroll
@@ -912,28 +935,25 @@ STL_HD bool verify_phase2_joint(const HalfState& p, const TableView& tab, Wide& 
     bool n0, n1;
     const int e0 = joint_index((dc - cr) >> 2, (dq - dr) >> 2, n0);
     const int e1 = joint_index(cr, dr, n1);
-    ge_cached c0, c1;
-    tab.load(e0, c0);  // both loads ahead of the doublings, as in verify_phase2_half
-    tab.load(e1, c1);
     if (bpos) wide.prefetch(de0, de1);
-    if (i != npos - 1) {
-      ge_p2_dbl<true>(t, acc2);
-      ge_p1p1_to_p2(acc2, t);
-      ge_p2_dbl(t, acc2);
-      ge_p1p1_to_p3(acc, t);
+    // the two sub-positions share one copy of the code (the loop body stays
+    // about the size of the two-table loop's): load the entry, two doublings
+    // while it arrives, one addition
+#pragma unroll 1
+    for (int sub = 0; sub < 2; ++sub) {
+      ge_cached c;
+      tab.load(sub == 0 ? e0 : e1, c);
+      if (sub == 1 || i != npos - 1) {
+        ge_p2_dbl<true>(t, acc2);
+        ge_p1p1_to_p2(acc2, t);
+        ge_p2_dbl(t, acc2);
+        ge_p1p1_to_p3(acc, t);
+      }
+      ge_cached_cneg(c, sub == 0 ? n0 : n1);
+      ge_add_cached(t, acc, c);
+      if (sub == 0 || !bpos) ge_p1p1_to_p2(acc2, t);
     }
-    ge_cached_cneg(c0, n0);
-    ge_add_cached(t, acc, c0);
-    ge_p1p1_to_p2(acc2, t);
-    ge_p2_dbl<true>(t, acc2);
-    ge_p1p1_to_p2(acc2, t);
-    ge_p2_dbl(t, acc2);
-    ge_p1p1_to_p3(acc, t);
-    ge_cached_cneg(c1, n1);
-    ge_add_cached(t, acc, c1);
-    if (!bpos) {
-      ge_p1p1_to_p2(acc2, t);
-    } else {
+    if (bpos) {
       ge_p1p1_to_p3(acc, t);
       wide.madd(t, acc, 0);
       ge_p1p1_to_p3(acc, t);

@@ -182,7 +182,10 @@ uint64_t hostemu_verify_batch_joint(const uint8_t* sig, const uint8_t* msg, cons
       ok = stl::verify_full_with_k(R, S, A, k, policy, tf, btab);
     } else {
       stl::WideHost wide{wide_tables(), {0, 0}};
-      ok = stl::verify_phase2_joint(hs, tj, wide);
+      static_assert(sizeof(stl::HalfState) == 14 * sizeof(uint4), "state");
+      uint4 st[14];
+      std::memcpy(st, &hs, sizeof(st));
+      ok = stl::verify_phase2_joint(st, tj, wide);
     }
     if (ok) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
   }
