@@ -866,67 +866,6 @@ STL_HD void build_joint_table(const TableView& tab, const uint4* state) {
   }
 }
 
-// Digits of verify_phase2_joint, one nibble position per next() from the
-// top (kHalfDigits - 1) down: c's and d's signed radix-16 digits and, at every
-// fourth position below 32, e's two radix-2^16 digits.  The same reads as
-// verify_phase2_half's loop head.
-struct JointDigits {
-  uint32_t cd[5], dd[5], ed[8];
-  uint32_t wc, wd, we0, we1;
-  int i;  // the position next() reads
-  STL_HD void init(const HalfState& p) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      cd[k] = p.cdig[k];
-      dd[k] = p.ddig[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ed[k] = p.edig[k];
-    wc = wd = we0 = we1 = 0;
-    i = kHalfDigits - 1;
-  }
-  STL_HD void next(int& dc, int& dq, bool& bpos, int& de0, int& de1) {
-    if ((i & 7) == 7) {
-      wc = cd[4];
-      wd = dd[4];
-#pragma unroll
-      for (int m = 4; m > 0; --m) {
-        cd[m] = cd[m - 1];
-        dd[m] = dd[m - 1];
-      }
-    }
-    if ((i & 7) == 4 && i < 32) {
-      we0 = ed[3];
-      we1 = ed[7];
-#pragma unroll
-      for (int m = 3; m > 0; --m) {
-        ed[m] = ed[m - 1];
-        ed[4 + m] = ed[4 + m - 1];
-      }
-    }
-    dc = (int32_t)wc >> 28;
-    dq = (int32_t)wd >> 28;
-    wc <<= 4;
-    wd <<= 4;
-    bpos = (i & 3) == 0 && i < 32;
-    de0 = de1 = 0;
-    if (bpos) {
-      de0 = (i & 4) ? (int32_t)we0 >> 16 : (int32_t)(we0 << 16) >> 16;
-      de1 = (i & 4) ? (int32_t)we1 >> 16 : (int32_t)(we1 << 16) >> 16;
-    }
-    --i;
-  }
-};
-
-// A nibble's radix-16 digits (dc, dq) -> the joint entries of its two
-// sub-positions: returns the high one's index (sign n0), the low one's in e1
-// (sign n1).
-STL_HD int joint_split(int dc, int dq, bool& n0, int& e1, bool& n1) {
-  const int cr = ((dc + 2) & 3) - 2, dr = ((dq + 2) & 3) - 2;
-  e1 = joint_index(cr, dr, n1);
-  return joint_index((dc - cr) >> 2, (dq - dr) >> 2, n0);
-}
-
 // Phase 2 with the joint table: [e]B + [c](-A) + [d](-Q) == O as in
 // verify_phase2_half (same digits, same wide-table madds at every fourth
 // nibble position, same identity test); one table, one add per sub-position.
@@ -947,65 +886,80 @@ STL_HD bool verify_phase2_joint(const uint4* state, const TableView& tab, Wide& 
     for (int i = 0; i < 20; ++i) w[i] = s[i];
   }
   const int npos = half_positions((int)(p.tops & 0xffu));
-  JointDigits ds;
-  ds.init(p);
-  int dc, dq, de0, de1;
-  bool bpos;
-  do {  // nibble positions above every lane's need hold zero digits
-    ds.next(dc, dq, bpos, de0, de1);
-  } while (ds.i >= npos - 1);
+  uint32_t cd[5], dd[5], ed[8];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    cd[i] = p.cdig[i];
+    dd[i] = p.ddig[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ed[i] = p.edig[i];
   ge_p3 acc;
   ge_p2 acc2;
   ge_p1p1 t;
   ge_p3_0(acc);
   ge_p2_0(acc2);
-  int e1;
-  bool n0, n1;
-  ge_cached ca, cb;
-  tab.load(joint_split(dc, dq, n0, e1, n1), ca);
-  // Software-pipelined over sub-positions: each entry is requested one
-  // sub-position (two doublings and an addition) before the two doublings that
-  // precede its own addition, as the two-table loop requested both of a
-  // nibble's entries ahead of its four doublings.
+  uint32_t wc = 0, wd = 0, we0 = 0, we1 = 0;
 #pragma unroll 1
-  for (int pos = npos - 1;; --pos) {
-    if (bpos) wide.prefetch(de0, de1);
-    tab.load(e1, cb);  // sub-position 1 of this nibble
-    if (pos != npos - 1) {
-      ge_p2_dbl<true>(t, acc2);
-      ge_p1p1_to_p2(acc2, t);
-      ge_p2_dbl(t, acc2);
-      ge_p1p1_to_p3(acc, t);
+  for (int i = kHalfDigits - 1; i >= 0; --i) {
+    if ((i & 7) == 7) {
+      wc = cd[4];
+      wd = dd[4];
+#pragma unroll
+      for (int m = 4; m > 0; --m) {
+        cd[m] = cd[m - 1];
+        dd[m] = dd[m - 1];
+      }
     }
-    ge_cached_cneg(ca, n0);
-    ge_add_cached(t, acc, ca);
-    ge_p1p1_to_p2(acc2, t);
-    int ndc = 0, ndq = 0, nde0 = 0, nde1 = 0, ne1 = 0;
-    bool nbpos = false, nn0 = false, nn1 = false;
-    if (pos > 0) ds.next(ndc, ndq, nbpos, nde0, nde1);  // wave-uniform
-    tab.load(joint_split(ndc, ndq, nn0, ne1, nn1), ca);  // sub-position 0 of the next nibble
-    ge_p2_dbl<true>(t, acc2);
-    ge_p1p1_to_p2(acc2, t);
-    ge_p2_dbl(t, acc2);
-    ge_p1p1_to_p3(acc, t);
-    ge_cached_cneg(cb, n1);
-    ge_add_cached(t, acc, cb);
-    if (!bpos) {
-      ge_p1p1_to_p2(acc2, t);
-    } else {
+    if ((i & 7) == 4 && i < 32) {
+      we0 = ed[3];
+      we1 = ed[7];
+#pragma unroll
+      for (int m = 3; m > 0; --m) {
+        ed[m] = ed[m - 1];
+        ed[4 + m] = ed[4 + m - 1];
+      }
+    }
+    const int dc = (int32_t)wc >> 28;
+    const int dq = (int32_t)wd >> 28;
+    wc <<= 4;
+    wd <<= 4;
+    const bool bpos = (i & 3) == 0 && i < 32;  // wave-uniform
+    int de0 = 0, de1 = 0;
+    if (bpos) {
+      de0 = (i & 4) ? (int32_t)we0 >> 16 : (int32_t)(we0 << 16) >> 16;
+      de1 = (i & 4) ? (int32_t)we1 >> 16 : (int32_t)(we1 << 16) >> 16;
+    }
+    if (i >= npos) continue;  // wave-uniform
+    const int cr = ((dc + 2) & 3) - 2, dr = ((dq + 2) & 3) - 2;
+    bool n0, n1;
+    const int e0 = joint_index((dc - cr) >> 2, (dq - dr) >> 2, n0);
+    const int e1 = joint_index(cr, dr, n1);
+    if (bpos) wide.prefetch(de0, de1);
+    // the two sub-positions share one copy of the code (the loop body stays
+    // about the size of the two-table loop's): load the entry, two doublings
+    // while it arrives, one addition
+#pragma unroll 1
+    for (int sub = 0; sub < 2; ++sub) {
+      ge_cached c;
+      tab.load(sub == 0 ? e0 : e1, c);
+      if (sub == 1 || i != npos - 1) {
+        ge_p2_dbl<true>(t, acc2);
+        ge_p1p1_to_p2(acc2, t);
+        ge_p2_dbl(t, acc2);
+        ge_p1p1_to_p3(acc, t);
+      }
+      ge_cached_cneg(c, sub == 0 ? n0 : n1);
+      ge_add_cached(t, acc, c);
+      if (sub == 0 || !bpos) ge_p1p1_to_p2(acc2, t);
+    }
+    if (bpos) {
       ge_p1p1_to_p3(acc, t);
       wide.madd(t, acc, 0);
       ge_p1p1_to_p3(acc, t);
       wide.madd(t, acc, 1);
       ge_p1p1_to_p2(acc2, t);
     }
-    if (pos == 0) break;
-    e1 = ne1;
-    n0 = nn0;
-    n1 = nn1;
-    bpos = nbpos;
-    de0 = nde0;
-    de1 = nde1;
   }
   fe ymz;
   fe_sub(ymz, acc2.Y, acc2.Z);
