@@ -282,12 +282,13 @@ struct Device {
   int ordinal = 0;
   int cus = 0;
   uint32_t grid = 0;  // resident workgroups for the verify kernel
-  hipStream_t stream = nullptr;  // kernels of the host batch API
-  hipStream_t copy = nullptr;    // its host-to-device copies (overlap the previous chunk's kernels)
-  ncclComm_t comm = nullptr;     // in-process communicator (rank = device index)
+  hipStream_t stream = nullptr;   // kernels of the host batch API (even chunks; results)
+  hipStream_t stream2 = nullptr;  // its odd chunks' kernels (g_tune_streams > 1)
+  hipStream_t copy = nullptr;     // its host-to-device copies (overlap the previous chunk's kernels)
+  ncclComm_t comm = nullptr;      // in-process communicator (rank = device index)
   std::mutex mu;
-  StreamCtx host;  // verify workspaces of the host batch API (on `stream`)
-  DevBuf sig, msg, pk, bitmap, pre, off, len, ctr, txid, status, wide, gather;
+  StreamCtx host, host2;  // verify workspaces of the host batch API (on `stream` / `stream2`)
+  DevBuf sig, msg, pk, bitmap, pre, off, len, ctr, ctr2, txid, status, wide, gather;
   DevBuf counters;  // device u64 counters of stl_get_stats: [0] accepted, [1] full-length lanes
   std::map<hipStream_t, std::unique_ptr<StreamCtx>> stream_ws;  // device-resident API
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;    // tx-hash work counter
@@ -377,6 +378,7 @@ int setup_device(Device& d) {
   if (per_cu < 1) per_cu = 1;
   d.grid = (uint32_t)(d.cus * per_cu);
   STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  STL_TRY(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
   STL_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
   STL_RC(d.counters.ensure(64));
   STL_TRY(hipMemsetAsync(d.counters.p, 0, 64, d.stream));
@@ -390,19 +392,22 @@ int setup_device(Device& d) {
 void release_device(Device& d) {
   (void)hipSetDevice(d.ordinal);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.stream2) (void)hipStreamSynchronize(d.stream2);
   if (d.copy) (void)hipStreamSynchronize(d.copy);
   if (d.comm && g_rccl.ok) (void)g_rccl.CommDestroy(d.comm);
   d.comm = nullptr;
-  for (DevBuf* b : {&d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.txid, &d.status,
+  for (DevBuf* b : {&d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.ctr2, &d.txid, &d.status,
                     &d.wide, &d.gather, &d.counters})
     b->release();
   d.host.release();
+  d.host2.release();
   for (auto& kv : d.stream_ws) kv.second->release();
   for (auto& kv : d.stream_ctr) kv.second->release();
   d.timer.release();
   if (d.stream) (void)hipStreamDestroy(d.stream);
+  if (d.stream2) (void)hipStreamDestroy(d.stream2);
   if (d.copy) (void)hipStreamDestroy(d.copy);
-  d.stream = d.copy = nullptr;
+  d.stream = d.stream2 = d.copy = nullptr;
 }
 
 int ensure_init() {
@@ -539,7 +544,7 @@ void shard_bytes_bounds(const uint32_t* len, size_t n, int g, std::vector<size_t
 // [watermark, max end of its rows), rebased on the shard's lowest offset, so
 // any offset order is correct.
 #ifndef STL_PIPE_CHUNK_LOG2
-#define STL_PIPE_CHUNK_LOG2 17  // 128K: one full round of resident main-kernel waves; A/B in DESIGN.md section 8
+#define STL_PIPE_CHUNK_LOG2 16  // 64K: two chunks' kernels share the chip (two streams); A/B in DESIGN.md section 8
 #endif
 constexpr size_t kPipeChunk = (size_t)1 << STL_PIPE_CHUNK_LOG2;
 
@@ -565,13 +570,13 @@ struct Shard {
   ~Shard() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   }
-  // Make d.stream wait for everything issued on d.copy so far.
-  int join_copy() {
+  // Make stream `to` wait for everything issued on `from` so far.
+  int join(hipStream_t from, hipStream_t to) {
     hipEvent_t e;
     STL_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ev.push_back(e);
-    STL_TRY(hipEventRecord(e, d->copy));
-    STL_TRY(hipStreamWaitEvent(d->stream, e, 0));
+    STL_TRY(hipEventRecord(e, from));
+    STL_TRY(hipStreamWaitEvent(to, e, 0));
     return STL_OK;
   }
 };
@@ -640,8 +645,18 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
   }
   uint8_t* dtxid = (b.mode == Mode::kBlob && b.txid) ? static_cast<uint8_t*>(d.txid.p) : nullptr;
   uint8_t* dstatus = b.mode == Mode::kBlob ? static_cast<uint8_t*>(d.status.p) : nullptr;
+  // Odd chunks' kernels go to d.stream2 (own verify workspace and hash work
+  // counter), so a chunk's phase 1 runs beside the previous chunk's main
+  // kernel, as the device-resident API's sub-chunks do.
+  // One stream while the phase clock is on: its per-kernel times must not
+  // overlap.
+  const bool two = g_tune_streams.load() > 1 && n > kPipeChunk && !phase_clock(d);
+  if (two && b.mode != Mode::kSig) STL_RC(d.ctr2.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
   for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
     const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
+    const bool odd = two && ((c0 / kPipeChunk) & 1);
+    hipStream_t ks = odd ? d.stream2 : d.stream;
+    uint32_t* kctr = static_cast<uint32_t*>((odd ? d.ctr2 : d.ctr).p);
     if (b.mode != Mode::kBlob) {
       STL_TRY(hipMemcpyAsync(dsig + 64 * c0, b.sig + 64 * (lo + c0), cn * 64, hipMemcpyHostToDevice, d.copy));
       STL_TRY(hipMemcpyAsync(dpk + 32 * c0, b.pk + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
@@ -650,17 +665,17 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
       STL_TRY(hipMemcpyAsync(dmsg + 32 * c0, b.msg32 + 32 * (lo + c0), cn * 32, hipMemcpyHostToDevice, d.copy));
     else
       STL_RC(copy_rows(s, dpre, b.bytes + base, c0, c1, &mark));
-    STL_RC(s.join_copy());
+    STL_RC(s.join(d.copy, ks));
     if (b.mode == Mode::kPre)
-      STL_TRY(stl::launch_tx_hash(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0,
-                                  static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream));
+      STL_TRY(stl::launch_tx_hash(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, kctr, hash_grid(d), ks));
     else if (b.mode == Mode::kBlob)
       STL_TRY(stl::launch_tx_blob(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, dsig + 64 * c0,
-                                  dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0,
-                                  static_cast<uint32_t*>(d.ctr.p), hash_grid(d), d.stream, b.kind));
-    STL_RC(run_verify(d, d.host, d.stream, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
+                                  dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0, kctr,
+                                  hash_grid(d), ks, b.kind));
+    STL_RC(run_verify(d, odd ? d.host2 : d.host, ks, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
                       static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, false, 1));
   }
+  if (two) STL_RC(s.join(d.stream2, d.stream));  // results are read on d.stream
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
   if (dtxid) STL_TRY(hipMemcpyAsync(b.txid + 32 * lo, dtxid, n * 32, hipMemcpyDeviceToHost, d.stream));
   return STL_OK;
@@ -672,7 +687,8 @@ int drain(Device& d) {
   (void)hipSetDevice(d.ordinal);
   const hipError_t a = hipStreamSynchronize(d.copy);
   const hipError_t b = hipStreamSynchronize(d.stream);
-  return (a == hipSuccess && b == hipSuccess) ? STL_OK : STL_EHIP;
+  const hipError_t c = hipStreamSynchronize(d.stream2);
+  return (a == hipSuccess && b == hipSuccess && c == hipSuccess) ? STL_OK : STL_EHIP;
 }
 
 // Per-device copy: the shard's bitmap words to the host bitmap bytes

@@ -139,6 +139,57 @@ def test_streams_with_caller_stream_and_phase_timing(stl, torch_cuda, batch):
         _apply(stl, old)
 
 
+def test_host_api_streams_same_bits(stl, torch_cuda, batch):
+    """The host batch API runs its 64K-signature chunks on one kernel stream,
+    or (streams > 1, the default) the odd chunks on a second stream with their
+    own verify workspace: same bits as the device API either way, with and
+    without key dedup (per-stream key tables)."""
+    torch = torch_cuda
+    n, d, host, rows, exp_golden, flip = batch
+    old = _apply(stl, SETTINGS[0])
+    try:
+        ref = _run(stl, torch, d, n)
+        ref_dedup = _run(stl, torch, d, n, stl.DEDUP_KEYS)
+        for streams in (1, 2):
+            stl.debug_tuning(stl.TUNE_STREAMS, streams)
+            assert np.array_equal(stl.verify_batch(*host), ref), streams
+            assert np.array_equal(stl.verify_batch(*host, policy=stl.DEDUP_KEYS), ref_dedup), streams
+    finally:
+        _apply(stl, old)
+
+
+def test_host_tx_api_streams_same_bits(stl, torch_cuda):
+    """stl_tx_verify_batch over 300,001 preimages (five 64K chunks: the
+    odd ones on the second stream with its own hash work counter): signatures
+    made on the GPU over SHA512Half of each preimage (hashlib), a 1 % sample
+    of rows signed over a different hash; same bits with one and two streams,
+    equal to the expectation."""
+    import hashlib
+    torch = torch_cuda
+    n = 300_001
+    rng = np.random.default_rng(31)
+    lens = rng.integers(100, 400, n)
+    blob = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8).tobytes()
+    offs = np.concatenate(([0], np.cumsum(lens)[:-1]))
+    pres = [b"STX\0" + blob[o:o + ln] for o, ln in zip(offs, lens)]
+    h = np.frombuffer(b"".join(hashlib.sha512(p).digest()[:32] for p in pres), np.uint8).reshape(n, 32).copy()
+    bad = rng.choice(n, n // 100, replace=False)
+    h[bad, 0] ^= 1
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pk, sig = stl.sign_batch_device(torch.from_numpy(seeds).cuda(), torch.from_numpy(h).cuda())
+    sig, pk = sig.cpu().numpy(), pk.cpu().numpy()
+    exp = np.ones(n, bool)
+    exp[bad] = False
+    old = stl.debug_tuning(stl.TUNE_STREAMS, 1)
+    try:
+        for streams in (1, 2):
+            stl.debug_tuning(stl.TUNE_STREAMS, streams)
+            got = stl.tx_verify_batch(pres, sig, pk)
+            assert np.array_equal(got, exp), (streams, np.nonzero(got != exp)[0][:8])
+    finally:
+        stl.debug_tuning(stl.TUNE_STREAMS, old)
+
+
 def test_tuning_rejects_bad_values(stl):
     from stellard_amd import _native as N
     lib = N.load()

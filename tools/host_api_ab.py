@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Host-API (PCIe-inclusive) rate of a libstl variant (STL_LIB_PATH):
-stl_ed25519_verify_batch on 1,048,576 host-resident signatures, median of 7."""
+stl_ed25519_verify_batch on 1,048,576 host-resident signatures (pageable numpy
+arrays, and pinned torch tensors as bench.py's end_to_end leg), median of 7."""
 import os
 import sys
 import time
@@ -27,4 +28,13 @@ for _ in range(7):
     ts.append(time.perf_counter() - t0)
 assert ok.all()
 t = float(np.median(ts))
-print(f"{os.path.basename(os.environ.get('STL_LIB_PATH', 'libstl.so'))}: host API {t * 1e3:.2f} ms  {n / t / 1e6:.1f} M/s")
+sp, mp, pp = (torch.from_numpy(a).pin_memory().numpy() for a in (s, m, p))
+tp = []
+for _ in range(7):
+    t0 = time.perf_counter()
+    ok = V.verify_batch(sp, mp, pp)
+    tp.append(time.perf_counter() - t0)
+assert ok.all()
+t2 = float(np.median(tp))
+print(f"{os.path.basename(os.environ.get('STL_LIB_PATH', 'libstl.so'))}: host API {t * 1e3:.2f} ms  {n / t / 1e6:.1f} M/s"
+      f"  pinned {t2 * 1e3:.2f} ms  {n / t2 / 1e6:.1f} M/s")
