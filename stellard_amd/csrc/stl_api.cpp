@@ -445,7 +445,8 @@ const stl::PhaseClock* phase_clock(Device& d);
 // stream per call, the library's own streams and events (created on first
 // use).  `streams` > 1 only for the device-resident API: the host batch API
 // already overlaps its copies with the previous chunk's kernels.
-int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode, int streams, stl::VerifyExec& x) {
+int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode, int streams, stl::VerifyExec& x,
+                bool concurrent = false) {
   const bool dedup = (mode & stl::kModeDedupKeys) != 0;
   x.grid = verify_grid_for(d, n);
   x.pair_max = pair_max(d);
@@ -454,6 +455,7 @@ int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode,
   x.clock = phase_clock(d);
   x.fused_prep = g_tune_fused.load();
   x.main_queue = g_tune_queue.load() != 0;
+  x.concurrent = concurrent;
   x.sub = 1u << g_tune_sub_log2.load();
   uint32_t S = (uint32_t)std::max(1, std::min<int>(streams, (int)stl::kMaxVerifyStreams));
   if (x.clock || n <= x.sub || x.sub <= x.pair_max) S = 1;
@@ -480,9 +482,10 @@ int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode,
 // streams are drained before returning (nothing may still run on the
 // caller's buffers outside the caller's stream).
 int run_verify(Device& d, StreamCtx& c, hipStream_t s, const uint8_t* sig, const uint8_t* msg_or_k,
-               const uint8_t* pk, size_t n, uint64_t* words, uint32_t mode, bool pre_k, int streams) {
+               const uint8_t* pk, size_t n, uint64_t* words, uint32_t mode, bool pre_k, int streams,
+               bool concurrent = false) {
   stl::VerifyExec x;
-  STL_RC(verify_exec(d, c, s, n, mode, streams, x));
+  STL_RC(verify_exec(d, c, s, n, mode, streams, x, concurrent));
   if (fault_now() || stl::launch_verify(sig, msg_or_k, pk, (uint32_t)n, words, mode, pre_k, x) != hipSuccess) {
     c.drain_aux();
     return STL_EHIP;
@@ -673,7 +676,7 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
                                   dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0, kctr,
                                   hash_grid(d), ks, b.kind));
     STL_RC(run_verify(d, odd ? d.host2 : d.host, ks, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
-                      static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, false, 1));
+                      static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, false, 1, two));
   }
   if (two) STL_RC(s.join(d.stream2, d.stream));  // results are read on d.stream
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));

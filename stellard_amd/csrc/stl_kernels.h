@@ -93,6 +93,8 @@ struct VerifyExec {
   int fused_prep = 1;                   // 0: scalar and point kernels; 1: phase 1 in one kernel;
                                         // 2: phase 1 inside the main kernel (verify_whole_kernel)
   bool main_queue = true;               // main kernel pulls 64-signature units from a counter
+  bool concurrent = false;              // other chunks share the chip (host API, two streams): no
+                                        // two-role phase 1 above pair_max (it trades work for latency)
   uint32_t nstreams = 1;
   uint32_t sub = kPreChunk;             // chunk size when nstreams > 1 (multiple of 64, >= 2^16)
   hipStream_t streams[kMaxVerifyStreams] = {};

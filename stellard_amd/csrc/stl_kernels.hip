@@ -1349,7 +1349,7 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
 #ifdef STL_POINT_PAIR_ALL
     const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup);
 #else
-    const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
+    const bool pair_point = pair || (!x.concurrent && (policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
 #endif
     const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
     if (x.fused_prep == 2 && !pair && !dedup) {
