@@ -122,7 +122,11 @@ typedef struct stl_config {
 } stl_config;
 
 /* Replaces/augments sodium_init() (src/ripple_app/ripple_app.cpp:129-132).
- * Idempotent; cfg may be NULL (all devices).  Thread-safe.  Environment
+ * Idempotent; cfg may be NULL (all devices).  Thread-safe.  When libstl is
+ * already running (an earlier stl_init, or the implicit one of a first entry-
+ * point call) a cfg still registers its fallback_verify and returns STL_OK if
+ * it asks for the live device set, gather mode and shard count, STL_EINVAL
+ * otherwise (stl_shutdown first to change them).  Environment
  * overrides: STL_DEVICES (device count), STL_SHARDS_PER_DEVICE, STL_RCCL
  * (1 = as STL_CFG_RCCL_GATHER, 0 = as STL_CFG_NO_RCCL), STL_FAULT_AFTER
  * (stl_debug_fault_after). */
@@ -141,7 +145,8 @@ const char *stl_strerror(int rc);
  * literal drop-in for `crypto_sign_verify_detached(...) == 0` at
  * RippleAddress.cpp:196-197: without one a device error must be told apart
  * from a reject by the caller (rc < -1).  STL_EINVAL (a NULL pointer) is
- * returned either way.
+ * returned either way; a message longer than 2^32 - 1 bytes is STL_EINVAL
+ * without a fallback and the fallback's answer (&& S < L) with one.
  * LATENCY: a signature is one GPU lane pair, so a call is latency-bound: 489 us
  * per call on MI355X against libsodium's 32 us, and concurrent calls
  * serialise on the device (tools/latency.py).
@@ -259,6 +264,16 @@ int stl_comm_info(int *nranks, int *rank);
  * Asynchronous on stream. */
 int stl_bitmap_gather_device(const uint64_t *d_words, size_t words_per_rank, uint64_t *d_all_words, int root,
                              void *stream);
+
+/* Variable-size gather (byte-balanced shards: config 5's ledger split by
+ * preimage bytes, stl_shard_range_bytes; or any unequal index shards): rank r
+ * holds d_words = word_offsets[r+1] - word_offsets[r] (= nwords) u64 words,
+ * which land at word word_offsets[r] of d_all_words on rank root.
+ * word_offsets: nranks+1 host entries, identical on every rank.  Grouped
+ * ncclSend / ncclRecv (the root's own slice is a device copy); asynchronous
+ * on stream.  STL_EINVAL if nwords disagrees with the offsets. */
+int stl_bitmap_gatherv_device(const uint64_t *d_words, size_t nwords, uint64_t *d_all_words,
+                              const uint64_t *word_offsets, int root, void *stream);
 
 /* Shard of [0, n) that rank r of g owns: contiguous, whole 64-signature
  * bitmap words (the layout stl_bitmap_gather_device assumes and the host

@@ -82,6 +82,7 @@ SYMBOLS = [
     ("stl_comm_destroy", None, []),
     ("stl_comm_info", ctypes.c_int, [_P, _P]),
     ("stl_bitmap_gather_device", ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_int, _P]),
+    ("stl_bitmap_gatherv_device", ctypes.c_int, [_P, ctypes.c_size_t, _P, _P, ctypes.c_int, _P]),
     ("stl_shard_range", None, [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _P, _P]),
     ("stl_shard_range_bytes", None, [_P, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _P, _P]),
     ("stl_debug_fault_after", None, [ctypes.c_longlong]),

@@ -840,14 +840,13 @@ extern "C" {
 
 int stl_init(const stl_config* cfg) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_init) return STL_OK;
-  const char* fa = std::getenv("STL_FAULT_AFTER");
-  if (fa && *fa) g_fault_after.store(std::atoll(fa));
-  g_trace = env_int("STL_TRACE", 0) != 0;
-  if (env_int("STL_PHASE_TIMING", 0) != 0) g_phase_timing.store(true);
-  // execution tuning from the environment (same ranges as stl_debug_tuning;
-  // profiling runs use STL_STREAMS=1 so that kernels do not overlap)
-  {
+  if (!g_init) {
+    const char* fa = std::getenv("STL_FAULT_AFTER");
+    if (fa && *fa) g_fault_after.store(std::atoll(fa));
+    g_trace = env_int("STL_TRACE", 0) != 0;
+    if (env_int("STL_PHASE_TIMING", 0) != 0) g_phase_timing.store(true);
+    // execution tuning from the environment (same ranges as stl_debug_tuning;
+    // profiling runs use STL_STREAMS=1 so that kernels do not overlap)
     const int s = env_int("STL_STREAMS", 0), c = env_int("STL_CHUNK_LOG2", 0);
     if (s >= 1 && s <= (int)stl::kMaxVerifyStreams) g_tune_streams.store(s);
     if (c >= 16 && c <= 20) g_tune_sub_log2.store(c);
@@ -869,12 +868,15 @@ int stl_init(const stl_config* cfg) {
       if (cfg->reserved != 0) return STL_EINVAL;
       if (cfg->shards_per_device > 0) spd = cfg->shards_per_device;
     }
-    // registered before any device is probed: a host without a usable
-    // device still answers single calls through it
+    // registered before any device is probed (a host without a usable device
+    // still answers single calls through it), and also when the library is
+    // already running -- e.g. started implicitly by a first entry-point call
+    // (ensure_init -> stl_init(NULL)) -- so that stl_ed25519_verify_detached
+    // keeps its 0 / -1 contract
     if (sz == sizeof(stl_config)) g_fallback_verify.store(cfg->fallback_verify);
   }
   int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return STL_ENODEV;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return g_init ? STL_OK : STL_ENODEV;
   if (want < 0) want = count;
   if (std::getenv("STL_DEVICES")) want = std::max(1, env_int("STL_DEVICES", want));
   spd = std::max(1, std::min(64, env_int("STL_SHARDS_PER_DEVICE", spd)));
@@ -883,6 +885,19 @@ int stl_init(const stl_config* cfg) {
   if (env_rccl == 0) cflags = (cflags & ~STL_CFG_RCCL_GATHER) | STL_CFG_NO_RCCL;
   if (first < 0 || first >= count) return STL_EINVAL;
   want = std::min(want, count - first);
+  // The in-process RCCL gather is opt-in (STL_CFG_RCCL_GATHER / STL_RCCL=1):
+  // every device copies its own slice to the host unless asked, until a
+  // multi-GPU run has shown the gathered bitmaps equal (ADVICE r2).
+  const bool gather = !(cflags & STL_CFG_NO_RCCL) && spd == 1 && (cflags & STL_CFG_RCCL_GATHER);
+  if (g_init) {
+    // idempotent for NULL or the live settings; a cfg asking for another
+    // device set, gather mode or shard count is refused rather than silently
+    // ignored (stl_shutdown first)
+    if (!cfg) return STL_OK;
+    const bool same = !g_devs.empty() && g_devs[0]->ordinal == first && (int)g_devs.size() == want &&
+                      gather == g_comm_gather && spd == g_shards_per_device;
+    return same ? STL_OK : STL_EINVAL;
+  }
   int prev = 0;
   (void)hipGetDevice(&prev);
   auto fail = [&](int rc) {
@@ -898,10 +913,6 @@ int stl_init(const stl_config* cfg) {
     const int rc = setup_device(*g_devs.back());
     if (rc) return fail(rc);
   }
-  // The in-process RCCL gather is opt-in (STL_CFG_RCCL_GATHER / STL_RCCL=1):
-  // every device copies its own slice to the host unless asked, until a
-  // multi-GPU run has shown the gathered bitmaps equal (ADVICE r2).
-  const bool gather = !(cflags & STL_CFG_NO_RCCL) && spd == 1 && (cflags & STL_CFG_RCCL_GATHER);
   if (gather) {
     if (!g_rccl.load() || fault_now()) return fail(STL_ERCCL);
     std::vector<ncclComm_t> comms(want);
@@ -1106,9 +1117,11 @@ bool s_lt_l(const uint8_t* S);
 
 int stl_ed25519_verify_detached(const uint8_t* sig, const uint8_t* m, unsigned long long mlen, const uint8_t* pk) {
   if (!sig || !pk || (mlen && !m)) return STL_EINVAL;
-  const int rc = verify_detached_device(sig, m, mlen, pk);
   const stl_verify_fn fb = g_fallback_verify.load();
-  if (rc >= -1 || rc == STL_EINVAL || fb == nullptr) return rc;
+  // a message longer than one device row (2^32 - 1 bytes) is valid input to
+  // libsodium: with a fallback registered it answers that case too
+  const int rc = mlen > 0xffffffffull ? STL_EINVAL : verify_detached_device(sig, m, mlen, pk);
+  if (rc >= -1 || fb == nullptr) return rc;
   // a device failure is never a reject: the caller's own check answers,
   // composed as RippleAddress::verifySignature composes it (RippleAddress.cpp:196-199)
   return (fb(sig, m, mlen, pk) == 0 && s_lt_l(sig + 32)) ? 0 : -1;
@@ -1339,6 +1352,38 @@ int stl_bitmap_gather_device(const uint64_t* d_words, size_t words_per_rank, uin
     STL_RCCL_TRY(g_rccl.Gather(d_words, d_all_words, words_per_rank, ncclUint64, root, g_pcomm, s));
   }
   return STL_OK;
+}
+
+int stl_bitmap_gatherv_device(const uint64_t* d_words, size_t nwords, uint64_t* d_all_words,
+                              const uint64_t* word_offsets, int root, void* stream) {
+  std::lock_guard<std::mutex> lk(g_pcomm_mu);
+  if (!g_pcomm) return STL_ERCCL;
+  if (!word_offsets || root < 0 || root >= g_pcomm_ranks) return STL_EINVAL;
+  int me = 0;
+  STL_RCCL_TRY(g_rccl.CommUserRank(g_pcomm, &me));
+  const int g = g_pcomm_ranks;
+  for (int r = 0; r < g; ++r)
+    if (word_offsets[r + 1] < word_offsets[r]) return STL_EINVAL;
+  if (word_offsets[me + 1] - word_offsets[me] != nwords || (nwords && !d_words)) return STL_EINVAL;
+  if (me == root && !d_all_words) return STL_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // the root's own slice: a device copy; every other non-empty slice: one
+  // send / recv pair at its word offset, all in one group
+  if (me == root && nwords)
+    STL_TRY(hipMemcpyAsync(d_all_words + word_offsets[me], d_words, nwords * 8, hipMemcpyDeviceToDevice, s));
+  STL_RCCL_TRY(g_rccl.GroupStart());
+  int rc = STL_OK;
+  if (me != root) {
+    if (nwords && g_rccl.Send(d_words, nwords, ncclUint64, root, g_pcomm, s) != ncclSuccess) rc = STL_ERCCL;
+  } else {
+    for (int r = 0; r < g; ++r) {
+      const size_t w = word_offsets[r + 1] - word_offsets[r];
+      if (r == root || w == 0) continue;
+      if (g_rccl.Recv(d_all_words + word_offsets[r], w, ncclUint64, r, g_pcomm, s) != ncclSuccess) rc = STL_ERCCL;
+    }
+  }
+  if (g_rccl.GroupEnd() != ncclSuccess && rc == STL_OK) rc = STL_ERCCL;
+  return rc;
 }
 
 }  // extern "C"

@@ -77,7 +77,14 @@ __device__ __forceinline__ void stage_base_table(uint32_t* sB, int tables) {
 // lane, in whole aligned lines from the start of the area, then the 16-B
 // tails, 2 x 9 quads per lane (the main kernel keeps its tails in LDS).  Entry
 // 0 is the identity; its head is kIdentityHead, shared by every lane.
+// Not const: a const __device__ array lives in the constant address space, and
+// TableView::head's select between it and the global workspace then became a
+// generic pointer, so every table read was a flat load (STL_ID_CONST: A/B).
+#ifdef STL_ID_CONST
 __device__ __attribute__((aligned(128))) const uint4 kIdentityHead[8] = {
+#else
+__device__ __attribute__((aligned(128))) uint4 kIdentityHead[8] = {
+#endif
     {1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 1u, 0u, 0u}, {0u, 0u, 0u, 0u},
     {0u, 0u, 1u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};  // YpX = YmX = Z = 1, T2d = 0
 __device__ __forceinline__ void lane_tables(uint4* ws, TableView& t1, TableView& t2) {

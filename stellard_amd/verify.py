@@ -457,6 +457,18 @@ def bitmap_gather_device(words, out_words=None, root=0, stream=None):
     return out_words
 
 
+def bitmap_gatherv_device(words, word_offsets, out_words=None, root=0, stream=None):
+    """stl_bitmap_gatherv_device: rank r's int64 words (word_offsets[r+1] -
+    word_offsets[r] of them) into out_words[word_offsets[r]:] on rank
+    ``root``; word_offsets has nranks+1 entries, the same on every rank."""
+    offs = np.ascontiguousarray(word_offsets, dtype=np.uint64)
+    ptr = ctypes.c_void_p(out_words.data_ptr()) if out_words is not None else None
+    wptr = ctypes.c_void_p(words.data_ptr()) if words.numel() else None
+    N.check(N.load().stl_bitmap_gatherv_device(wptr, words.numel(), ptr, _buf(offs), root, _stream_ptr(stream)),
+            "stl_bitmap_gatherv_device")
+    return out_words
+
+
 # ---- statistics (include/stl.h stl_get_stats) ----
 
 class Stats(ctypes.Structure):

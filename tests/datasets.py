@@ -12,6 +12,16 @@ bitmaps against those digests).
              pre-reject), chunks of 2,000,000 with seed 0x5EED0004 + offset
   config 3   67,108,864 signatures, same construction, chunks of 4,194,304
              with seed 0x5EED0003 + chunk offset
+  config 5   one ledger of 2^20 signed preimages ("STX\0" + random bytes,
+             lengths log-uniform in [113, 4096]), 1,000 signers, 2 % of the
+             rows made invalid after signing (a bit of the preimage, of R or
+             of S), seed 0x5EED0005 (ledger_plan below)
+
+Block digests: besides the whole-config digests, make_digests.py commits a
+SHA-256 (first 16 bytes) of the inputs and of the expected bitmap of every
+block of BLOCK = 65,536 rows (tests/golden/block_digests.json), so that each
+rank of a sharded run can check its own slice -- ranks own whole blocks
+(block_shard) -- before rank 0 checks the gathered bitmap's digest.
 
 Row construction (per chunk): rng = default_rng(seed); seeds = 32 random
 bytes per row, msgs = 32 random bytes per row; (pk, sig) = RFC 8032 keypair
@@ -30,7 +40,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-import ed25519_py as ed  # noqa: E402
 
 CONFIGS = {
     "config2": {"n": 1 << 20, "chunk": 1 << 20, "seed": 0x5EED0002, "frac": 0.0},
@@ -39,6 +48,9 @@ CONFIGS = {
 }
 
 DIGESTS = os.path.join(ROOT, "tests", "golden", "bitmap_digests.json")
+BLOCK_DIGESTS = os.path.join(ROOT, "tests", "golden", "block_digests.json")
+BLOCK = 1 << 16
+CONFIG5 = {"n": 1 << 20, "seed": 0x5EED0005, "signers": 1000, "frac": 0.02, "len_min": 113, "len_max": 4096}
 
 CLASSES = ["valid", "B1_msg_bit", "B2_R_bit", "B3_S_bit", "B4_S_plus_L", "B5_S_top_bits", "B6_small_order_pk",
            "B7_small_order_R", "B8_mixed_order_pk", "B9_noncanonical_pk", "B10_pk_not_on_curve",
@@ -46,9 +58,17 @@ CLASSES = ["valid", "B1_msg_bit", "B2_R_bit", "B3_S_bit", "B4_S_plus_L", "B5_S_t
 NCLASSES = len(CLASSES) - 1
 
 
+def _ed():
+    # the pure-Python restatement is only needed to build rows on the host
+    # (make_digests.py, the CPU tests); the bench builds them on the device
+    import ed25519_py
+    return ed25519_py
+
+
 def _small_order_encodings():
     """The 14 encodings of points of order dividing 8 (both sign bits, y = p
     and p + 1), sorted -- kSmallOrderEnc on the device."""
+    ed = _ed()
     tors, _ = ed.torsion_points()
     so = set()
     for t in tors:
@@ -61,19 +81,31 @@ def _small_order_encodings():
     return sorted(so)
 
 
-SMALL_ORDER = _small_order_encodings()
-TORSION = [ed.encode(t) for t in ed.torsion_points()[0]]  # i * T8, kTorsionEnc
+_CONST = {}
+
+
+def _const(name):
+    if not _CONST:
+        ed = _ed()
+        _CONST["SMALL_ORDER"] = _small_order_encodings()
+        _CONST["TORSION"] = [ed.encode(t) for t in ed.torsion_points()[0]]  # i * T8, kTorsionEnc
+    return _CONST[name]
+
+
 NONCANON_R = [bytes.fromhex(h) for h in ("ee" + "ff" * 30 + "7f", "01" + "00" * 30 + "80", "ee" + "ff" * 30 + "ff")]
 S_TOP = (0xE0, 0x80, 0x40, 0x20)
 
 
 def _k_times_a(R, A, M, a):
+    ed = _ed()
     return (ed.sha512_int(R, A, M) % ed.L) * a % ed.L
 
 
 def mutate_row(c, u, seed, A, sig, M, group):
     """Class-c mutation with parameter u of one honest row (bytes) -> (A, sig,
     M).  group: (scalarmult_base(S) -> 32 B, point_add(P, Q) -> 32 B)."""
+    ed = _ed()
+    SMALL_ORDER, TORSION = _const("SMALL_ORDER"), _const("TORSION")
     R, S = bytearray(sig[:32]), bytearray(sig[32:])
     A, M = bytearray(A), bytearray(M)
     byte, bit = u % 32, 1 << ((u >> 5) & 7)
@@ -124,6 +156,7 @@ def mutate_row(c, u, seed, A, sig, M, group):
 
 def python_group():
     """Group operations in pure Python (slow; for small cross-checks)."""
+    ed = _ed()
     return (lambda S: ed.encode(ed.mul(int.from_bytes(S, "little"), ed.B)),
             lambda P, Q: ed.encode(ed.add(ed.decode(P), ed.decode(Q))))
 
@@ -219,3 +252,109 @@ class Digest:
     def result(self):
         return {"rows": self.rows, "accepted": self.accepted, "bitmap_sha256": self.bits.hexdigest(),
                 "inputs_sha256": self.inputs.hexdigest()}
+
+
+# ---------------------------------------------------------------- blocks
+def h16(*arrays):
+    """First 16 bytes (hex) of SHA-256 over the arrays' bytes, in order."""
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()[:32]
+
+
+class BlockDigest:
+    """Per-BLOCK digests of a row stream fed chunk by chunk (chunks need not
+    be block aligned): inputs = h16(sig, msg, pk of the block's rows), bitmap =
+    h16(packbits of the block's accept bits, LSB first)."""
+
+    def __init__(self):
+        self.inputs, self.bitmap = [], []
+        self._rows = []  # pending (sig, msg, pk, bits) pieces of the current block
+        self._n = 0
+
+    def add(self, sig, msg, pk, bits):
+        i = 0
+        n = bits.shape[0]
+        while i < n:
+            take = min(BLOCK - self._n, n - i)
+            self._rows.append((sig[i:i + take], msg[i:i + take], pk[i:i + take], bits[i:i + take]))
+            self._n += take
+            i += take
+            if self._n == BLOCK:
+                self._emit()
+
+    def _emit(self):
+        if not self._n:
+            return
+        parts = list(zip(*self._rows))
+        sig, msg, pk, bits = (np.concatenate(p) for p in parts)
+        self.inputs.append(h16(sig, msg, pk))
+        self.bitmap.append(h16(np.packbits(np.asarray(bits, bool), bitorder="little")))
+        self._rows, self._n = [], 0
+
+    def result(self):
+        self._emit()
+        return {"block_rows": BLOCK, "inputs_h16": self.inputs, "bitmap_h16": self.bitmap}
+
+
+def block_shard(n, rank, world):
+    """Rows [lo, hi) of rank `rank` of `world` when ranks own whole BLOCKs,
+    as evenly as blocks allow (the last block may be partial): block range
+    [rank*B // world, (rank+1)*B // world) of B = ceil(n / BLOCK) blocks."""
+    nb = -(-n // BLOCK)
+    b0, b1 = rank * nb // world, (rank + 1) * nb // world
+    return min(n, b0 * BLOCK), min(n, b1 * BLOCK), b0, b1
+
+
+def rows_plan(name, lo, hi):
+    """The dataset pieces covering rows [lo, hi) of a config:
+    yields (row0, seeds, msgs, cls, param) slices of the chunk plans (each
+    chunk's plan is built whole -- it is one rng stream -- and cut)."""
+    for c0, seed, n, frac in chunks(name):
+        a, b = max(lo, c0), min(hi, c0 + n)
+        if a >= b:
+            continue
+        seeds, msgs, cls, param = chunk_plan(seed, n, frac)
+        yield a, seeds[a - c0:b - c0], msgs[a - c0:b - c0], cls[a - c0:b - c0], param[a - c0:b - c0]
+
+
+# ---------------------------------------------------------------- config 5
+def ledger_plan(cfg=CONFIG5):
+    """One synthetic ledger: signing preimages packed
+    back to back ("STX\\0" || random bytes, lengths log-uniform), the signer
+    seed of every row, and the rows made invalid after signing with their
+    kind (0 = a preimage bit, 1 = an R bit, 2 = an S bit) and parameter."""
+    rng = np.random.default_rng(cfg["seed"])
+    n = cfg["n"]
+    lens = np.exp(rng.uniform(np.log(cfg["len_min"]), np.log(cfg["len_max"]), n)).astype(np.int32)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.int64)
+    total = int(offs[-1] + lens[-1])
+    pre = rng.integers(0, 256, total + 16, dtype=np.uint8)  # 16 B of tail padding: the hash kernel's loads
+    for j, b in enumerate(b"STX\x00"):
+        pre[offs + j] = b
+    signers = rng.integers(0, 256, (cfg["signers"], 32), dtype=np.uint8)
+    who = rng.integers(0, cfg["signers"], n)
+    bad = np.sort(rng.choice(n, int(n * cfg["frac"]), replace=False))
+    kind = (np.arange(bad.size) % 3).astype(np.uint8)
+    param = rng.integers(0, 1 << 32, bad.size, dtype=np.uint64)
+    return {"n": n, "pre": pre, "total": total, "offs": offs, "lens": lens, "signers": signers, "who": who,
+            "bad": bad, "kind": kind, "param": param}
+
+
+def ledger_mutations(lp):
+    """Where the invalid rows' bits flip: (preimage byte positions, xor bytes)
+    and (signature rows, byte columns, xor bytes) -- applied after signing."""
+    bad, kind, u = lp["bad"], lp["kind"], lp["param"]
+    bit = (np.uint64(1) << ((u >> np.uint64(16)) & np.uint64(7))).astype(np.uint8)
+    k0 = kind == 0
+    rows0 = bad[k0]
+    pos = lp["offs"][rows0] + 4 + (u[k0] % (lp["lens"][rows0] - 4).astype(np.uint64)).astype(np.int64)
+    ks = ~k0
+    col = (u[ks] % np.uint64(32)).astype(np.int64) + np.where(kind[ks] == 2, 32, 0)
+    return (pos, bit[k0]), (bad[ks], col, bit[ks])
+
+
+def ledger_input_digest(pre, total, lens, sig, pk):
+    return h16(pre[:total], lens.astype("<i4"), sig, pk)

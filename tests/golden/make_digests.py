@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
 """Generates tests/golden/bitmap_digests.json: SHA-256 digests of the accept
 bitmaps libsodium 1.0.18 gives the seeded datasets of BASELINE.json configs 2,
-4 and 3 (tests/datasets.py), with the digests of the inputs.
+4, 3 and 5 (tests/datasets.py), with the digests of the inputs; and
+tests/golden/block_digests.json: the same per 65,536-row block (inputs and
+expected bitmap, first 16 bytes of SHA-256), which each rank of a sharded
+bench run checks its own slice against.  Where a config's whole-input or
+bitmap digest is already committed the regenerated one must equal it.
 
 Run here (the build container: libsodium at /opt/conda/lib), never on the GPU
 box.  Signing and verification both go through oracle/_ref/libsodium_ref.so
 (crypto_sign_seed_keypair + crypto_sign_detached, and the reference's
 verifySignature = crypto_sign_verify_detached && S < L).
 
-    python tests/golden/make_digests.py [config2 config4 config3]
+    python tests/golden/make_digests.py [config2 config4 config3 config5]
 """
 import json
 import os
@@ -23,6 +27,59 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from tests import datasets, oracle_bind  # noqa: E402
 
 
+def _store_block(name, blocks):
+    doc = {}
+    if os.path.exists(datasets.BLOCK_DIGESTS):
+        with open(datasets.BLOCK_DIGESTS) as f:
+            doc = json.load(f)
+    doc[name] = blocks
+    with open(datasets.BLOCK_DIGESTS, "w") as f:
+        json.dump(doc, f, indent=0, sort_keys=True)
+
+
+def _check_same(out, name, got):
+    old = out.get(name)
+    if old:
+        for k in ("inputs_sha256", "bitmap_sha256", "accepted", "rows"):
+            if k in old and k in got:
+                assert old[k] == got[k], (name, k, old[k], got[k])
+
+
+def config5(lib, threads):
+    """The ledger of datasets.ledger_plan: SHA512Half of every preimage
+    (hashlib), libsodium signing by each row's signer, the invalid rows'
+    bit flips, SHA512Half again where a preimage changed, libsodium's
+    verifySignature."""
+    import hashlib
+    lp = datasets.ledger_plan()
+    n, pre, offs, lens = lp["n"], lp["pre"], lp["offs"], lp["lens"]
+    mv = memoryview(pre)
+
+    def half(rows):
+        return np.frombuffer(b"".join(hashlib.sha512(mv[int(offs[i]):int(offs[i] + lens[i])]).digest()[:32]
+                                      for i in rows), np.uint8).reshape(-1, 32)
+    msgs = half(range(n)).copy()
+    pk, sig = oracle_bind.sodium_sign_batch(lib, np.ascontiguousarray(lp["signers"][lp["who"]]), msgs, threads)
+    (pos, pbit), (srow, scol, sbit) = datasets.ledger_mutations(lp)
+    pre[pos] ^= pbit
+    sig[srow, scol] ^= sbit
+    changed = np.unique(np.searchsorted(offs, pos, side="right") - 1)
+    msgs[changed] = half(changed)
+    bits = oracle_bind.sodium_verify_batch(lib, sig, msgs, pk, threads)
+    bm = np.packbits(bits.astype(bool), bitorder="little")
+    import hashlib as hl
+    return {"rows": n, "accepted": int(bits.sum()), "bitmap_sha256": hl.sha256(bm.tobytes()).hexdigest(),
+            "inputs_h16": datasets.ledger_input_digest(pre, lp["total"], lens, sig, pk),
+            "preimage_bytes": lp["total"], "invalid_rows": int(lp["bad"].size),
+            "invalid_by_kind": {k: int((lp["kind"] == i).sum()) for i, k in
+                                enumerate(("preimage_bit", "R_bit", "S_bit"))},
+            **{k: v for k, v in datasets.CONFIG5.items()},
+            "construction": "datasets.ledger_plan: one ledger, signed over SHA512Half(preimage), invalid rows' "
+                            "bits flipped after signing",
+            "expected_from": f"libsodium {lib.ref_sodium_version().decode()} crypto_sign_verify_detached && S < L "
+                             "over SHA512Half (hashlib) of each preimage"}
+
+
 def main(names):
     lib = oracle_bind.load_sodium_ref()
     assert lib is not None, "needs libsodium"
@@ -34,7 +91,16 @@ def main(names):
     group = datasets.sodium_group(lib)
     for name in names:
         t0 = time.time()
+        if name == "config5":
+            got = config5(lib, threads)
+            _check_same(out, name, got)
+            out[name] = got
+            with open(datasets.DIGESTS, "w") as f:
+                json.dump(out, f, indent=1, sort_keys=True)
+            print(f"config5: {got['accepted']} accepted ({time.time() - t0:.0f} s)", flush=True)
+            continue
         dg = datasets.Digest()
+        blk = datasets.BlockDigest()
         classes, keys = {}, []
 
         def make(seeds, msgs, cls, param):
@@ -47,22 +113,27 @@ def main(names):
             sig, msg, pk, cls = datasets.chunk(seed, n, frac, make)
             bits = oracle_bind.sodium_verify_batch(lib, sig, msg, pk, threads)
             dg.add(sig, msg, pk, bits)
+            blk.add(sig, msg, pk, bits)
             for k, v in datasets.class_counts(cls).items():
                 classes[k] = classes.get(k, 0) + v
             adv = np.nonzero(cls)[0]
             keys.append(datasets.row_keys(sig[adv], msg[adv], pk[adv]))
             print(f"{name}: rows {c0 + n} accepted {dg.accepted} ({time.time() - t0:.0f} s)", flush=True)
         keys = np.concatenate(keys) if keys else np.zeros(0, "S16")
-        out[name] = dict(dg.result(), **datasets.CONFIGS[name], adversarial_rows_by_class=classes,
-                         adversarial_rows_distinct=int(np.unique(keys).size),
-                         construction="each adversarial row mutated from its own honest row, classes B1-B11 "
-                                      "evenly (tests/datasets.py)",
-                         expected_from=f"libsodium {lib.ref_sodium_version().decode()} "
-                                       "crypto_sign_verify_detached && S < L")
+        got = dict(dg.result(), **datasets.CONFIGS[name], adversarial_rows_by_class=classes,
+                   adversarial_rows_distinct=int(np.unique(keys).size),
+                   construction="each adversarial row mutated from its own honest row, classes B1-B11 "
+                                "evenly (tests/datasets.py)",
+                   expected_from=f"libsodium {lib.ref_sodium_version().decode()} "
+                                 "crypto_sign_verify_detached && S < L")
+        _check_same(out, name, got)
+        out[name] = got
         with open(datasets.DIGESTS, "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)
-    print(json.dumps(out, indent=1))
+        _store_block(name, blk.result())
+    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "adversarial_rows_by_class"}
+                      for k, v in out.items()}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["config2", "config4", "config3"])
+    main(sys.argv[1:] or ["config2", "config4", "config3", "config5"])

@@ -535,3 +535,83 @@ def test_comm_info(stl):
         stl.comm_destroy()
     with reinit(stl, flags=N.STL_CFG_RCCL_GATHER):
         assert stl.comm_info() == (1, 0)
+
+
+def test_fallback_registered_after_implicit_init(stl, oracle, golden):
+    """a first entry-point call starts libstl implicitly
+    (stl_init(NULL)); a later stl_init(cfg) must still register cfg's
+    fallback -- not return early -- so verify_detached keeps returning only
+    0 / -1 under injected device faults.  A cfg asking for other live settings
+    (here the RCCL gather) is refused, not ignored.  A message longer than one
+    device row (mlen > 2^32 - 1, valid input to libsodium) goes to the
+    fallback too, composed with S < L."""
+    import ctypes
+
+    from stellard_amd import _native as N
+    sig, msg, pk, exp = _golden_rows(golden, 12, seed=23)
+    lib = N.load()
+    seen = []
+
+    def fb(s, m, mlen, p):
+        seen.append(mlen)
+        if mlen > 0xFFFFFFFF:
+            return 0  # stands in for libsodium hashing a huge message; never reads m
+        return 0 if oracle.verify_raw(ctypes.string_at(s, 64), ctypes.string_at(m, mlen),
+                                      ctypes.string_at(p, 32), policy=0) else -1
+
+    fn = stl.VERIFY_FN(fb)
+    stl.shutdown()
+    try:
+        rc = lib.stl_ed25519_verify_detached(sig[0].tobytes(), msg[0].tobytes(), 32, pk[0].tobytes())
+        assert rc == (0 if exp[0] else -1)  # implicit init
+        stl.init(fallback_verify=fn)  # already running: registers the fallback
+        for i in range(12):
+            for k in range(0, 6):
+                stl.debug_fault_after(k)
+                rc = lib.stl_ed25519_verify_detached(sig[i].tobytes(), msg[i].tobytes(), 32, pk[i].tobytes())
+                stl.debug_fault_after(-1)
+                assert rc in (0, -1) and (rc == 0) == bool(exp[i]), (i, k, rc)
+        assert 32 in seen
+        with pytest.raises(N.StlError) as e:
+            stl.init(flags=N.STL_CFG_RCCL_GATHER, fallback_verify=fn)
+        assert e.value.rc == N.STL_EINVAL
+        stl.init(fallback_verify=fn)  # the live settings: idempotent
+        big = 1 << 33
+        good = sig[int(np.argmax(exp))].tobytes()
+        rc = lib.stl_ed25519_verify_detached(good, msg[0].tobytes(), big, pk[0].tobytes())
+        assert rc == 0 and seen[-1] == big
+        s_plus_l = good[:32] + (int.from_bytes(good[32:], "little") + L).to_bytes(32, "little")
+        assert lib.stl_ed25519_verify_detached(s_plus_l, msg[0].tobytes(), big, pk[0].tobytes()) == -1
+    finally:
+        stl.debug_fault_after(-1)
+        stl.shutdown()
+        stl.init()
+    # without a fallback the oversized message is an argument error
+    assert lib.stl_ed25519_verify_detached(sig[0].tobytes(), msg[0].tobytes(), 1 << 33, pk[0].tobytes()) == N.STL_EINVAL
+
+
+def test_bitmap_gatherv_one_rank(stl, torch_cuda):
+    """stl_bitmap_gatherv_device on a one-rank communicator (the 1-GPU box):
+    the root's slice lands at its word offset by a device copy; counts that
+    disagree with the offsets are refused.  The N > 1 send/recv legs run in
+    bench.py's config-4 / config-5 legs on a multi-GPU node."""
+    torch = torch_cuda
+    from stellard_amd import _native as N
+    words = torch.arange(1, 1001, dtype=torch.int64, device="cuda") * 0x0101010101
+    full = torch.zeros(1000, dtype=torch.int64, device="cuda")
+    stl.comm_init_rank(1, 0, stl.comm_unique_id())
+    try:
+        stl.bitmap_gatherv_device(words, [0, 1000], full, root=0)
+        torch.cuda.synchronize()
+        assert torch.equal(full, words)
+        with pytest.raises(N.StlError) as e:
+            stl.bitmap_gatherv_device(words[:999], [0, 1000], full, root=0)
+        assert e.value.rc == N.STL_EINVAL
+        with pytest.raises(N.StlError) as e:
+            stl.bitmap_gatherv_device(words, [0, 1000], full, root=1)
+        assert e.value.rc == N.STL_EINVAL
+    finally:
+        stl.comm_destroy()
+    with pytest.raises(N.StlError) as e:  # no communicator
+        stl.bitmap_gatherv_device(words, [0, 1000], full, root=0)
+    assert e.value.rc == N.STL_ERCCL

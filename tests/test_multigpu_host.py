@@ -53,6 +53,77 @@ def test_bench_launcher_dry_run(gpus):
     assert line["metric"].startswith("DRY RUN")
 
 
+@pytest.mark.parametrize("gpus,fault", [(1, None), (2, None), (4, None), (2, "shift"), (2, "dup"), (4, "zero")])
+def test_bench_digest_rehearsal_catches_bad_gather(gpus, fault):
+    """the multi-rank legs must be able to FAIL.  The dry run
+    runs tools/bench_legs.py's sharding (whole 65,536-row blocks, unequal at
+    10M rows), gather and digest check over gloo with a fixed accept pattern;
+    shifting rank 1's words, replacing them with rank 0's slice or zeroing them
+    must turn digest_equal false, the clean run must keep it true."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dry-run", "--steps", "1",
+           "--warmup", "0", "--per-gpu", "4096"]
+    if fault:
+        cmd += ["--dry-run-fault", fault]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    leg = _last_json(r.stdout)["extra_configs"]["digest_rehearsal"]
+    assert leg["n_ranks"] == gpus and leg["rows"] == 10_000_000
+    assert leg["unequal_shards"] == (gpus > 1)
+    assert leg["digest_equal"] is (fault is None or gpus == 1), leg
+
+
+def test_block_shards_cover_and_align():
+    """datasets.block_shard: contiguous, covering, whole 65,536-row blocks
+    (word aligned), and the word offsets bench_legs gathers at."""
+    from tests import datasets
+    for n in (1 << 20, 10_000_000, 1 << 26, 65_536 * 3 + 17):
+        for world in (1, 2, 3, 4, 8):
+            prev = 0
+            for r in range(world):
+                lo, hi, b0, b1 = datasets.block_shard(n, r, world)
+                assert lo == prev and lo % datasets.BLOCK == 0 and lo % 64 == 0
+                assert hi == min(n, b1 * datasets.BLOCK) and lo == min(n, b0 * datasets.BLOCK)
+                prev = hi
+            assert prev == n
+
+
+def test_block_digests_committed_and_consistent():
+    """tests/golden/block_digests.json (libsodium-built, make_digests.py)
+    covers every block of configs 2-4 and agrees with the whole-config
+    digests' row counts; config 5's ledger digest is committed too."""
+    from tests import datasets
+    with open(datasets.BLOCK_DIGESTS) as f:
+        blocks = json.load(f)
+    with open(datasets.DIGESTS) as f:
+        whole = json.load(f)
+    for name in ("config2", "config4", "config3"):
+        nb = -(-datasets.CONFIGS[name]["n"] // datasets.BLOCK)
+        assert blocks[name]["block_rows"] == datasets.BLOCK
+        assert len(blocks[name]["inputs_h16"]) == len(blocks[name]["bitmap_h16"]) == nb
+        assert whole[name]["rows"] == datasets.CONFIGS[name]["n"]
+    c5 = whole["config5"]
+    assert c5["rows"] == datasets.CONFIG5["n"] and c5["accepted"] == c5["rows"] - c5["invalid_rows"]
+
+
+def test_ledger_plan_and_mutations():
+    """datasets.ledger_plan is deterministic; the invalid rows' flips land
+    inside their own preimage (after the 4-byte prefix) or signature."""
+    from tests import datasets
+    cfg = dict(datasets.CONFIG5, n=4096)
+    a, b = datasets.ledger_plan(cfg), datasets.ledger_plan(cfg)
+    assert all(np.array_equal(a[k], b[k]) for k in ("pre", "offs", "lens", "who", "bad", "param"))
+    assert (a["lens"] >= 113).all() and (a["lens"] <= 4096).all()
+    assert all(bytes(a["pre"][o:o + 4]) == b"STX\x00" for o in a["offs"][:50])
+    (pos, pbit), (srow, scol, sbit) = datasets.ledger_mutations(a)
+    rows = np.searchsorted(a["offs"], pos, side="right") - 1
+    assert set(rows.tolist()) <= set(a["bad"].tolist())
+    assert ((pos - a["offs"][rows]) >= 4).all() and (pos < a["offs"][rows] + a["lens"][rows]).all()
+    assert (scol >= 0).all() and (scol < 64).all() and (pbit > 0).all() and (sbit > 0).all()
+    assert pos.size + srow.size == a["bad"].size
+
+
 def test_bench_rank_count_must_match():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],

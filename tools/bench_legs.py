@@ -1,0 +1,354 @@
+"""Sharded, digest-checked legs of bench.py (BASELINE.json configs[2]-[4]).
+
+Each leg runs at every N with one rank per GPU and proves bit-exactness of
+the *gathered* result, not only of each rank's own slice:
+
+  config3_64M_digest       configs[2]: the 67,108,864-row dataset of
+                           tests/datasets.py (2 % adversarial rows over the
+                           Appendix-B classes B1-B11), index shards of whole
+                           65,536-row blocks, ncclGather to rank 0
+                           (stl_bitmap_gather_device);
+  config4_10M_digest       configs[3]: the 10,000,000-row adversarial set, the
+                           same block shards -- unequal at N = 2, 4, 8 (153
+                           blocks, the last one partial) -- gathered with
+                           stl_bitmap_gatherv_device;
+  config5_ledger_split     configs[4]: ONE ledger of 2^20 signed preimages
+                           (113 B - 4 KB, 1,000 signers, 2 % invalid rows) split
+                           by preimage bytes (stl_shard_range_bytes), SHA512Half +
+                           verify per rank, stl_bitmap_gatherv_device.
+
+Every rank rebuilds only its own rows (the device signer and adversarial-row
+builder, stl_debug_sign_adversarial_device, from the seeded plans), checks its
+inputs against the committed per-block digests (tests/golden/
+block_digests.json, made with libsodium by tests/golden/make_digests.py),
+verifies, checks its slice's per-block bitmap digests, and rank 0 compares
+the SHA-256 of the gathered bitmap with libsodium's
+(tests/golden/bitmap_digests.json).  A misplaced, duplicated, missing or
+stale rank slice changes that digest (tests/test_multigpu_host.py shifts one
+rank's words in the CPU rehearsal and expects digest_equal false).
+
+The predicate sharded here is RippleAddress::verifySignature
+(/root/reference/src/ripple_data/protocol/RippleAddress.cpp:190-200); the
+batch split over ranks replaces the JobQueue worker pool
+(src/ripple_core/functional/JobQueue.cpp:217-243) and, for config 5, one
+ledger's transaction set (src/ripple_app/consensus/LedgerConsensus.cpp:1934-1958).
+"""
+import hashlib
+import json
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from tests import datasets
+
+
+def bitmap_sha256(full_words, n):
+    """SHA-256 of the first n accept bits as packed bytes (LSB first), the
+    form of tests/golden/bitmap_digests.json."""
+    arr = full_words.cpu().numpy() if hasattr(full_words, "cpu") else np.asarray(full_words)
+    b = arr.astype("<i8").view(np.uint8)[:(n + 7) // 8].copy()
+    if n % 8:
+        b[-1] &= (1 << (n % 8)) - 1
+    return hashlib.sha256(b.tobytes()).hexdigest()
+
+
+def words_h16(words):
+    arr = words.cpu().numpy() if hasattr(words, "cpu") else np.asarray(words)
+    return datasets.h16(arr.astype("<i8"))
+
+
+class Gather:
+    """Accept-bitmap words of every rank into one buffer on rank 0.
+
+    mode "rccl": libstl (ncclGather when every slice has the same word count,
+    grouped send / recv -- stl_bitmap_gatherv_device -- otherwise); "nccl":
+    torch.distributed's RCCL all_gather of padded slices (used only if libstl's
+    communicator could not be built); "gloo": through host memory (the
+    multi-rank rehearsal on a 1-GPU box and the CPU dry run); world 1: the
+    rank's own words."""
+
+    def __init__(self, world, rank, dist, mode, V=None, stream=None, group=None):
+        self.world, self.rank, self.dist, self.mode = world, rank, dist, mode
+        self.V, self.stream, self.group = V, stream, group
+
+    def __call__(self, words, offs, full):
+        """words: this rank's slice (offs[rank+1] - offs[rank] int64 words);
+        offs: world+1 word offsets; full: offs[-1] words on rank 0 (else None)."""
+        import torch
+        if self.world == 1:
+            if full is not None and full.data_ptr() != words.data_ptr():
+                full[:words.numel()].copy_(words)
+            return
+        sizes = [int(offs[r + 1] - offs[r]) for r in range(self.world)]
+        equal = len(set(sizes)) == 1
+        if self.mode == "rccl":
+            if equal:
+                self.V.bitmap_gather_device(words, full, root=0, stream=self.stream)
+            else:
+                self.V.bitmap_gatherv_device(words, offs, full, root=0, stream=self.stream)
+            return
+        mx = max(sizes)
+        pad = torch.zeros(mx, dtype=torch.int64, device=words.device if self.mode == "nccl" else "cpu")
+        pad[:words.numel()].copy_(words)
+        parts = [torch.empty_like(pad) for _ in range(self.world)]
+        if self.mode == "nccl":
+            self.dist.all_gather(parts, pad, group=self.group)
+        else:
+            self.dist.all_gather(parts, pad)
+        if self.rank == 0:
+            for r in range(self.world):
+                full[int(offs[r]):int(offs[r + 1])].copy_(parts[r][:sizes[r]])
+
+
+def _all(dist, world, obj):
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def timed(ctx, fn, reps):
+    """Median over reps of (barrier, fn, sync, barrier) on this rank, max over
+    ranks (seconds)."""
+    import torch
+    world, dist = ctx["world"], ctx["dist"]
+    ts = []
+    for _ in range(reps):
+        ctx["sync"]()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        fn()
+        ctx["sync"]()
+        if world > 1:
+            dist.barrier()
+        ts.append(time.perf_counter() - t0)
+    t = torch.tensor([float(np.median(ts))], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+class _BlockInputs:
+    """Streams rows (from row `lo`, block aligned) into per-block input
+    digests, hashed on a thread pool (hashlib releases the GIL)."""
+
+    def __init__(self, pool):
+        self.pool, self.pending, self.n, self.futs = pool, [], 0, []
+
+    def add(self, sig, msg, pk):
+        i, n = 0, sig.shape[0]
+        while i < n:
+            take = min(datasets.BLOCK - self.n, n - i)
+            self.pending.append((sig[i:i + take], msg[i:i + take], pk[i:i + take]))
+            self.n += take
+            i += take
+            if self.n == datasets.BLOCK:
+                self._emit()
+
+    def _emit(self):
+        if self.n:
+            s, m, p = (np.concatenate(x) for x in zip(*self.pending))
+            self.futs.append(self.pool.submit(datasets.h16, s, m, p))
+        self.pending, self.n = [], 0
+
+    def result(self):
+        self._emit()
+        return [f.result() for f in self.futs]
+
+
+def digest_leg(ctx, name, reps=3):
+    """configs[2] / configs[3] on this rank's block shard; see the module
+    docstring.  ctx: world, rank, dist, V, torch, dev, stream, sync, gather."""
+    torch, V, dev, stream = ctx["torch"], ctx["V"], ctx["dev"], ctx["stream"]
+    world, rank = ctx["world"], ctx["rank"]
+    n = datasets.CONFIGS[name]["n"]
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)[name]
+    with open(datasets.BLOCK_DIGESTS) as f:
+        blocks = json.load(f)[name]
+    lo, hi, b0, b1 = datasets.block_shard(n, rank, world)
+    offs = np.array([datasets.block_shard(n, r, world)[0] // 64 for r in range(world)] + [(n + 63) // 64],
+                    np.uint64)
+    m = hi - lo
+    err, inputs_ok = None, False
+    try:
+        sig = torch.empty((m, 64), dtype=torch.uint8, device=dev)
+        msg = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+        pk = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+        t0 = time.time()
+        with ThreadPoolExecutor(8) as pool:
+            bi = _BlockInputs(pool)
+            for a, seeds, msgs, cls, param in datasets.rows_plan(name, lo, hi):
+                k = seeds.shape[0]
+                t = [torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+                     for x in (seeds, msgs, cls, param.view(np.int32))]
+                p_, s_, m_ = V.sign_adversarial_device(*t)
+                sig[a - lo:a - lo + k] = s_
+                msg[a - lo:a - lo + k] = m_
+                pk[a - lo:a - lo + k] = p_
+                bi.add(s_.cpu().numpy(), m_.cpu().numpy(), p_.cpu().numpy())
+            got_in = bi.result()
+        build_s = time.time() - t0
+        inputs_ok = got_in == blocks["inputs_h16"][b0:b1]
+        words = torch.zeros((m + 63) // 64, dtype=torch.int64, device=dev)
+        full = torch.zeros(int(offs[-1]), dtype=torch.int64, device=dev) if rank == 0 else None
+        if world > 1 and ctx["gather"].mode == "gloo" and rank == 0:
+            full = full.cpu()
+        V.verify_batch_device(sig, msg, pk, out_words=words, stream=stream)
+        ctx["sync"]()
+        bits = V.words_to_bool(words, m)
+        got_bits = [datasets.h16(np.packbits(bits[i:i + datasets.BLOCK], bitorder="little"))
+                    for i in range(0, m, datasets.BLOCK)]
+        slice_ok = got_bits == blocks["bitmap_h16"][b0:b1]
+    except Exception as e:  # noqa: BLE001 - every rank learns of it before the leg's collectives
+        err = f"rank {rank}: {e!r}"
+    fault = ctx.get("fault")
+    st = _all(ctx["dist"], world, (err, bool(inputs_ok)))
+    if any(e for e, _ in st):
+        return {"error": "; ".join(e for e, _ in st if e)}
+    if not all(o for _, o in st):
+        return {"error": f"input block digests differ on ranks {[r for r, (_, o) in enumerate(st) if not o]}"}
+
+    def step():
+        V.verify_batch_device(sig, msg, pk, out_words=words, stream=stream)
+        if fault:
+            fault(words)
+        ctx["gather"](words, offs, full)
+
+    dt = timed(ctx, step, reps)
+    slices = _all(ctx["dist"], world, {"rank": rank, "rows": [lo, hi], "slice_bitmap_blocks_equal": bool(slice_ok),
+                                       "accepted": int(bits.sum())})
+    out = {"rows": n, "n_ranks": world, "verifies_per_s": n / dt, "ms": dt * 1e3, "median_of": reps,
+           "shards": "whole 65,536-row blocks per rank (datasets.block_shard), "
+                     + ("equal: ncclGather" if len(set(np.diff(offs.astype(np.int64)))) == 1 or world == 1
+                        else "unequal: grouped send/recv (stl_bitmap_gatherv_device)"),
+           "rank_slices": slices, "build_s": build_s,
+           "data": "tests/datasets.py %s, rows rebuilt per rank by the device signer + adversarial-row builder, "
+                   "inputs checked per 65,536-row block against libsodium-built digests" % name,
+           "timing": "barrier, one verify call per rank over its resident rows + gather to rank 0, sync, "
+                     "barrier; median, max over ranks"}
+    if rank == 0:
+        dg = bitmap_sha256(full, n)
+        acc = int(np.unpackbits(full.cpu().numpy().astype("<i8").view(np.uint8), bitorder="little")[:n].sum())
+        out.update({"accepted": acc, "accepted_expected": want["accepted"],
+                    "bitmap_sha256": dg, "digest_equal": dg == want["bitmap_sha256"],
+                    "expected_from": want.get("expected_from")})
+    return out
+
+
+def ledger_leg(ctx, reps=5):
+    """configs[4]: one ledger split across the ranks by preimage bytes."""
+    torch, V, dev, stream = ctx["torch"], ctx["V"], ctx["dev"], ctx["stream"]
+    world, rank = ctx["world"], ctx["rank"]
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)["config5"]
+    err, inputs = None, None
+    try:
+        t0 = time.time()
+        lp = datasets.ledger_plan()
+        n = lp["n"]
+        d_pre = torch.from_numpy(lp["pre"]).to(dev)
+        d_off = torch.from_numpy(lp["offs"]).to(dev)
+        d_len = torch.from_numpy(lp["lens"]).to(dev)
+        seeds = torch.from_numpy(np.ascontiguousarray(lp["signers"][lp["who"]])).to(dev)
+        msgs = V.tx_hash_batch_device(d_pre, d_off, d_len, stream=stream)
+        pk, sig = V.sign_batch_device(seeds, msgs)
+        (pos, pbit), (srow, scol, sbit) = datasets.ledger_mutations(lp)
+        d_pre[torch.from_numpy(pos).to(dev)] ^= torch.from_numpy(pbit).to(dev)
+        sig[torch.from_numpy(srow).to(dev), torch.from_numpy(scol).to(dev)] ^= torch.from_numpy(sbit).to(dev)
+        ctx["sync"]()
+        inputs = datasets.ledger_input_digest(d_pre.cpu().numpy(), lp["total"], lp["lens"], sig.cpu().numpy(),
+                                              pk.cpu().numpy())
+        build_s = time.time() - t0
+        bounds = [V.shard_range_bytes(lp["lens"], r, world) for r in range(world)]
+        lo, hi = bounds[rank]
+        offs = np.array([b[0] // 64 for b in bounds] + [(n + 63) // 64], np.uint64)
+        m = hi - lo
+        m5 = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        words = torch.zeros((m + 63) // 64, dtype=torch.int64, device=dev)
+        full = torch.zeros(int(offs[-1]), dtype=torch.int64, device=dev) if rank == 0 else None
+        if world > 1 and ctx["gather"].mode == "gloo" and rank == 0:
+            full = full.cpu()
+    except Exception as e:  # noqa: BLE001 - every rank learns of it before the leg's collectives
+        err = f"rank {rank}: {e!r}"
+    st = _all(ctx["dist"], world, (err, inputs == want["inputs_h16"]))
+    if any(e for e, _ in st):
+        return {"error": "; ".join(e for e, _ in st if e)}
+    if not all(o for _, o in st):
+        return {"error": f"ledger input digest differs on ranks {[r for r, (_, o) in enumerate(st) if not o]}"}
+
+    def step(flags):
+        if m:
+            V.tx_hash_batch_device(d_pre, d_off[lo:hi], d_len[lo:hi], out_msg=m5[lo:hi], stream=stream)
+            V.verify_batch_device(sig[lo:hi], m5[lo:hi], pk[lo:hi], out_words=words, policy=flags, stream=stream)
+        ctx["gather"](words, offs, full)
+
+    step(0)
+    ctx["sync"]()
+    res = {}
+    for label, flags in (("", 0), ("_dedup_keys", V.DEDUP_KEYS)):
+        dt = timed(ctx, lambda: step(flags), reps)  # noqa: B023 - called right here
+        res["tx_per_s" + label] = n / dt
+        res["ms" + label] = dt * 1e3
+        if rank == 0:
+            res["digest_equal" + label] = bitmap_sha256(full, n) == want["bitmap_sha256"]
+    pre_bytes = [int(lp["offs"][b[1] - 1] + lp["lens"][b[1] - 1] - lp["offs"][b[0]]) if b[1] > b[0] else 0
+                 for b in bounds]
+    out = {"transactions": n, "n_ranks": world, "scaling": "strong (one ledger split across the ranks)",
+           "preimage_bytes": lp["total"], "byte_shards": [list(map(int, b)) for b in bounds],
+           "preimage_bytes_per_rank": pre_bytes, "median_of": reps, "build_s": build_s, **res,
+           "invalid_rows": int(lp["bad"].size),
+           "data": "tests/datasets.py ledger_plan: 'STX\\0' + random bytes, lengths log-uniform in [113, 4096], "
+                   "1,000 signers, GPU-signed over SHA512Half, 2 % of the rows with a preimage / R / S bit "
+                   "flipped after signing; every rank builds the whole ledger and checks its input digest",
+           "timing": "barrier, SHA512Half + verify of the rank's byte shard + gather to rank 0 "
+                     "(stl_bitmap_gatherv_device), sync, barrier; median, max over ranks"}
+    if rank == 0:
+        out.update({"accepted_expected": want["accepted"], "bitmap_sha256_expected": want["bitmap_sha256"]})
+    return out
+
+
+def _pattern_bits(lo, hi):
+    """Dry-run stand-in for a verifier: a fixed, irregular accept pattern of
+    rows [lo, hi) (about 2 % rejects), identical whoever computes it."""
+    i = np.arange(lo, hi, dtype=np.uint64)
+    h = (i * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(57)
+    return h >= np.uint64(3)
+
+
+def _pack_words(bits):
+    b = np.packbits(bits, bitorder="little")
+    b = np.concatenate([b, np.zeros(-len(b) % 8, np.uint8)])
+    return b.view("<i8")
+
+
+def dry_digest_leg(ctx, n=10_000_000, fault=None):
+    """CPU rehearsal of digest_leg's sharding, gather and digest check (no GPU,
+    no verification): every rank packs the fixed pattern of its block shard,
+    `fault` ("shift" / "dup" / "zero") corrupts rank 1's slice the way a wrong
+    gather offset, a duplicated rank-0 slice or a skipped rank would, and rank
+    0 compares the gathered digest with the pattern's over all n rows."""
+    import torch
+    world, rank = ctx["world"], ctx["rank"]
+    lo, hi, b0, b1 = datasets.block_shard(n, rank, world)
+    offs = np.array([datasets.block_shard(n, r, world)[0] // 64 for r in range(world)] + [(n + 63) // 64],
+                    np.uint64)
+    words = torch.from_numpy(_pack_words(_pattern_bits(lo, hi)).copy())
+    if fault and rank == min(1, world - 1):
+        if fault == "shift":
+            words = torch.roll(words, 1)
+        elif fault == "dup":
+            words = torch.from_numpy(_pack_words(_pattern_bits(0, hi - lo)).copy())
+        elif fault == "zero":
+            words = torch.zeros_like(words)
+    full = torch.zeros(int(offs[-1]), dtype=torch.int64) if rank == 0 else None
+    dt = timed(ctx, lambda: ctx["gather"](words, offs, full), 3)
+    out = {"rows": n, "n_ranks": world, "ms": dt * 1e3, "fault": fault,
+           "unequal_shards": len(set(np.diff(offs.astype(np.int64)).tolist())) > 1}
+    if rank == 0:
+        want = hashlib.sha256(np.packbits(_pattern_bits(0, n), bitorder="little").tobytes()).hexdigest()
+        out["digest_equal"] = bitmap_sha256(full, n) == want
+    return out

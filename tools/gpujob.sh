@@ -1,0 +1,60 @@
+#!/bin/bash
+# One parameterised GPU-box job (replaces the per-session gpu_r0*.sh scripts).
+#
+#   tools/gpujob.sh OUT STEP [STEP ...]
+#
+# Runs from the repo root on the GPU box; every step writes under
+# gpurun_out/OUT and has its own time limit; the job stops at the first
+# failing step (no retries).  Steps:
+#   suite              pytest -m gpu (the round-end suite)
+#   smoke              __graft_entry__.smoke()
+#   bench              python bench.py (defaults: the driver's N = 1 line)
+#   bench2             bench.py --gpus 2 --gather gloo (multi-rank rehearsal on one GPU)
+#   profile            tools/profile.sh: kernel trace + FETCH/WRITE/SQ PMC passes
+#   valu               tools/valu_pmc.sh: VALUBusy / INT64 / occupancy PMC passes
+#   ab:K:R:V1,V2       ABBA of libstl builds build/ab/V.so ("base" = stellard_amd/libstl.so),
+#                      tools/exec_ab.py K launches x R rotations per run, serial + 2-stream
+#   py:SCRIPT[:ARGS]   python3 tools/SCRIPT ARGS (comma-separated ARGS), stdout to OUT/SCRIPT.log
+set -o pipefail
+OUT=$1; shift
+[ -n "$OUT" ] || { echo "usage: tools/gpujob.sh OUT STEP..."; exit 2; }
+D=gpurun_out/$OUT
+mkdir -p $D
+export TMPDIR=/tmp
+
+run() {  # run NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  local t0=$(date +%s)
+  timeout -k 10 $secs "$@" > $D/$name.log 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc $(( $(date +%s) - t0 )) s"
+  tail -2 $D/$name.log
+  return $rc
+}
+
+for step in "$@"; do
+  case $step in
+    suite) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit $? ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) run bench 600 python -u bench.py || exit $? ;;
+    bench2) run bench_n2_rehearsal 600 python -u bench.py --gpus 2 --gather gloo --no-cpu-baseline || exit $? ;;
+    profile) run profile 900 bash tools/profile.sh $OUT/prof || exit $? ;;
+    valu) run valu 900 bash tools/valu_pmc.sh $OUT/valu || exit $? ;;
+    ab:*)
+      IFS=: read -r _ K R VS <<< "$step"
+      IFS=, read -r -a vs <<< "$VS"
+      order=("${vs[@]}")
+      for ((i=${#vs[@]}-1; i>=0; i--)); do order+=("${vs[$i]}"); done
+      for v in "${order[@]}" "${order[@]}"; do
+        lib=""; [ "$v" != base ] && lib=build/ab/$v.so
+        STL_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/exec_ab.py $K $R s1=1,1,1,18 s2=1,1,2,18 \
+          >> $D/var_$v.jsonl 2>> $D/var_$v.err
+        rc=$?; echo "variant $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    py:*)
+      IFS=: read -r _ S A <<< "$step"
+      run ${S%.py} 600 python3 -u tools/$S ${A//,/ } || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "gpujob $OUT done"
