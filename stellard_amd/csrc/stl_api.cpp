@@ -249,26 +249,20 @@ std::atomic<int> g_tune_streams{2};   // concurrent streams per device-resident 
 std::atomic<int> g_tune_sub_log2{18}; // signatures per stream chunk
 std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
 
-// Verify workspaces of one caller stream: ws[0] for the caller's stream, and
-// with several streams per call (g_tune_streams) ws[j] for the library's own
-// stream aux[j], forked from and joined to the caller's by events.
+// The verify workspace of one stream: every launch that runs kernels on a
+// stream uses that stream's workspace, in stream order -- the caller's streams
+// (device-resident API) and the library's own pool streams alike, so a pool
+// stream shared by several callers and both APIs needs only one.  `mu` is
+// held while a launch is planned and enqueued (the workspace may grow).
 struct StreamCtx {
-  DevBuf ws[stl::kMaxVerifyStreams];
-  hipStream_t aux[stl::kMaxVerifyStreams] = {};
+  std::mutex mu;
+  DevBuf ws;
+  // fork / join events of launches whose chunks this (caller) stream spreads
+  // over pool streams
   hipEvent_t fork = nullptr;
   hipEvent_t join[stl::kMaxVerifyStreams] = {};
-  // Wait for everything issued on the library's streams (error paths).
-  void drain_aux() {
-    for (hipStream_t s : aux)
-      if (s) (void)hipStreamSynchronize(s);
-  }
   void release() {
-    drain_aux();
-    for (auto& b : ws) b.release();
-    for (hipStream_t& s : aux) {
-      if (s) (void)hipStreamDestroy(s);
-      s = nullptr;
-    }
+    ws.release();
     for (hipEvent_t& e : join) {
       if (e) (void)hipEventDestroy(e);
       e = nullptr;
@@ -278,23 +272,28 @@ struct StreamCtx {
   }
 };
 
+// Streams ("stream pool"): HIP maps the streams of a
+// process onto GPU_MAX_HW_QUEUES (4 on the pool) hardware queues in creation
+// order, and two streams on one queue run one after another.  So libstl makes
+// exactly three streams per device, in stl_init, in a fixed order -- two
+// kernel streams and one copy stream -- and both APIs share them: the host
+// batch API runs even / odd chunks on `stream` / `stream2` and copies on
+// `copy`; a device-resident call runs its chunks on the caller's stream plus
+// `stream2` (then `stream`).  Made before the caller's later streams, they
+// keep their own queues whatever the caller creates afterwards.
 struct Device {
   int ordinal = 0;
   int cus = 0;
   uint32_t grid = 0;  // resident workgroups for the verify kernel
-  hipStream_t stream = nullptr;   // kernels of the host batch API (even chunks; results)
-  // its odd chunks' kernels (g_tune_streams > 1), created at the first host
-  // batch that uses it: HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware
-  // queues, and one created up front took the queue the device-resident API's
-  // second stream needs, serialising its chunks (bench 8.76 vs 8.44 ms)
-  hipStream_t stream2 = nullptr;
-  hipStream_t copy = nullptr;     // its host-to-device copies (overlap the previous chunk's kernels)
+  hipStream_t stream = nullptr;   // kernel stream 0: host batch API even chunks and results
+  hipStream_t stream2 = nullptr;  // kernel stream 1: host API odd chunks; a device call's second stream
+  hipStream_t copy = nullptr;     // host-to-device copies (overlap the previous chunk's kernels)
+  hipStream_t stream3 = nullptr;  // a device call's fourth stream (STL_TUNE_STREAMS 4 only; made on use)
   ncclComm_t comm = nullptr;      // in-process communicator (rank = device index)
   std::mutex mu;
-  StreamCtx host, host2;  // verify workspaces of the host batch API (on `stream` / `stream2`)
   DevBuf sig, msg, pk, bitmap, pre, off, len, ctr, ctr2, txid, status, wide, gather;
   DevBuf counters;  // device u64 counters of stl_get_stats: [0] accepted, [1] full-length lanes
-  std::map<hipStream_t, std::unique_ptr<StreamCtx>> stream_ws;  // device-resident API
+  std::map<hipStream_t, std::unique_ptr<StreamCtx>> stream_ws;  // workspace of every stream used
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;    // tx-hash work counter
   std::mutex ws_mu;
   PhaseTimer timer;
@@ -381,7 +380,9 @@ int setup_device(Device& d) {
   STL_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stl::kernel_verify_msg32(), stl::kBlock, 0));
   if (per_cu < 1) per_cu = 1;
   d.grid = (uint32_t)(d.cus * per_cu);
+  // the stream pool, in this order (see Device)
   STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  STL_TRY(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
   STL_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
   STL_RC(d.counters.ensure(64));
   STL_TRY(hipMemsetAsync(d.counters.p, 0, 64, d.stream));
@@ -394,23 +395,19 @@ int setup_device(Device& d) {
 
 void release_device(Device& d) {
   (void)hipSetDevice(d.ordinal);
-  if (d.stream) (void)hipStreamSynchronize(d.stream);
-  if (d.stream2) (void)hipStreamSynchronize(d.stream2);
-  if (d.copy) (void)hipStreamSynchronize(d.copy);
+  for (hipStream_t s : {d.stream, d.stream2, d.stream3, d.copy})
+    if (s) (void)hipStreamSynchronize(s);
   if (d.comm && g_rccl.ok) (void)g_rccl.CommDestroy(d.comm);
   d.comm = nullptr;
   for (DevBuf* b : {&d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.ctr2, &d.txid, &d.status,
                     &d.wide, &d.gather, &d.counters})
     b->release();
-  d.host.release();
-  d.host2.release();
   for (auto& kv : d.stream_ws) kv.second->release();
   for (auto& kv : d.stream_ctr) kv.second->release();
   d.timer.release();
-  if (d.stream) (void)hipStreamDestroy(d.stream);
-  if (d.stream2) (void)hipStreamDestroy(d.stream2);
-  if (d.copy) (void)hipStreamDestroy(d.copy);
-  d.stream = d.stream2 = d.copy = nullptr;
+  for (hipStream_t s : {d.stream, d.stream2, d.stream3, d.copy})
+    if (s) (void)hipStreamDestroy(s);
+  d.stream = d.stream2 = d.stream3 = d.copy = nullptr;
 }
 
 int ensure_init() {
@@ -421,7 +418,7 @@ int ensure_init() {
   return stl_init(nullptr);
 }
 
-// Verify workspaces for (device, stream) pairs used by the device-resident API.
+// The verify workspace of stream s on device d (created on first use).
 StreamCtx& stream_ctx(Device& d, hipStream_t s) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
   auto& slot = d.stream_ws[s];
@@ -443,14 +440,18 @@ uint32_t pair_max(const Device& d) { return d.grid * stl::kBlock / 4; }
 unsigned long long* dev_counters(Device& d);
 const stl::PhaseClock* phase_clock(Device& d);
 
-// Execution plan of one launch_verify of n signatures on stream s: the
-// workspaces of context c (allocated on first use) and, with more than one
-// stream per call, the library's own streams and events (created on first
-// use).  `streams` > 1 only for the device-resident API: the host batch API
-// already overlaps its copies with the previous chunk's kernels.
-int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode, int streams, stl::VerifyExec& x,
-                bool concurrent = false) {
+// Plans and enqueues one launch_verify of n signatures on stream s: with
+// `streams` > 1 (device-resident API only: the host batch API already overlaps
+// its copies with the previous chunk's kernels) chunks also go to the pool
+// streams stream2, stream, stream3 (the caller's own stream excluded), forked
+// from and joined to s by s's events.  Every stream involved contributes its
+// workspace; their mutexes are held (in address order) until the launch is
+// enqueued.  On an error the pool streams used are drained before returning
+// (nothing may still run on the caller's buffers outside the caller's stream).
+int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, size_t n,
+               uint64_t* words, uint32_t mode, bool pre_k, int streams, bool concurrent = false) {
   const bool dedup = (mode & stl::kModeDedupKeys) != 0;
+  stl::VerifyExec x;
   x.grid = verify_grid_for(d, n);
   x.pair_max = pair_max(d);
   x.wide = static_cast<const uint4*>(d.wide.p);
@@ -463,34 +464,39 @@ int verify_exec(Device& d, StreamCtx& c, hipStream_t s, size_t n, uint32_t mode,
   uint32_t S = (uint32_t)std::max(1, std::min<int>(streams, (int)stl::kMaxVerifyStreams));
   if (x.clock || n <= x.sub || x.sub <= x.pair_max) S = 1;
   S = (uint32_t)std::min<size_t>(S, (n + x.sub - 1) / x.sub);
-  x.nstreams = S;
-  for (uint32_t j = 0; j < S; ++j) {
-    STL_RC(c.ws[j].ensure(stl::verify_ws_bytes(d.grid, dedup)));
-    x.ws[j] = static_cast<uint4*>(c.ws[j].p);
-    if (j == 0) {
-      x.streams[0] = s;
-      continue;
+  hipStream_t pool[stl::kMaxVerifyStreams] = {s};
+  uint32_t np = 1;
+  if (S > 1) {
+    if (S > 3 && !d.stream3) {
+      std::lock_guard<std::mutex> lk(d.ws_mu);
+      if (!d.stream3) STL_TRY(hipStreamCreateWithFlags(&d.stream3, hipStreamNonBlocking));
     }
-    if (!c.aux[j]) STL_TRY(hipStreamCreateWithFlags(&c.aux[j], hipStreamNonBlocking));
-    if (!c.join[j]) STL_TRY(hipEventCreateWithFlags(&c.join[j], hipEventDisableTiming));
-    x.streams[j] = c.aux[j];
-    x.join[j] = c.join[j];
+    for (hipStream_t p : {d.stream2, d.stream, d.stream3})
+      if (np < S && p && p != s) pool[np++] = p;
+  }
+  S = np;
+  x.nstreams = S;
+  StreamCtx* ctx[stl::kMaxVerifyStreams];
+  for (uint32_t j = 0; j < S; ++j) ctx[j] = &stream_ctx(d, pool[j]);
+  StreamCtx* order[stl::kMaxVerifyStreams];
+  std::copy(ctx, ctx + S, order);
+  std::sort(order, order + S);
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (uint32_t j = 0; j < S; ++j) locks.emplace_back(order[j]->mu);
+  StreamCtx& c = *ctx[0];
+  for (uint32_t j = 0; j < S; ++j) {
+    STL_RC(ctx[j]->ws.ensure(stl::verify_ws_bytes(d.grid, dedup)));
+    x.ws[j] = static_cast<uint4*>(ctx[j]->ws.p);
+    x.streams[j] = pool[j];
+    if (j > 0) {
+      if (!c.join[j]) STL_TRY(hipEventCreateWithFlags(&c.join[j], hipEventDisableTiming));
+      x.join[j] = c.join[j];
+    }
   }
   if (S > 1 && !c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
   x.fork = c.fork;
-  return STL_OK;
-}
-
-// launch_verify with the plan of verify_exec; on an error the library's own
-// streams are drained before returning (nothing may still run on the
-// caller's buffers outside the caller's stream).
-int run_verify(Device& d, StreamCtx& c, hipStream_t s, const uint8_t* sig, const uint8_t* msg_or_k,
-               const uint8_t* pk, size_t n, uint64_t* words, uint32_t mode, bool pre_k, int streams,
-               bool concurrent = false) {
-  stl::VerifyExec x;
-  STL_RC(verify_exec(d, c, s, n, mode, streams, x, concurrent));
   if (fault_now() || stl::launch_verify(sig, msg_or_k, pk, (uint32_t)n, words, mode, pre_k, x) != hipSuccess) {
-    c.drain_aux();
+    for (uint32_t j = 1; j < S; ++j) (void)hipStreamSynchronize(pool[j]);
     return STL_EHIP;
   }
   return STL_OK;
@@ -657,7 +663,6 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
   // One stream while the phase clock is on: its per-kernel times must not
   // overlap.
   const bool two = g_tune_streams.load() > 1 && n > kPipeChunk && !phase_clock(d);
-  if (two && !d.stream2) STL_TRY(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
   if (two && b.mode != Mode::kSig) STL_RC(d.ctr2.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
   for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
     const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
@@ -679,7 +684,7 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
       STL_TRY(stl::launch_tx_blob(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, dsig + 64 * c0,
                                   dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0, kctr,
                                   hash_grid(d), ks, b.kind));
-    STL_RC(run_verify(d, odd ? d.host2 : d.host, ks, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
+    STL_RC(run_verify(d, ks, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
                       static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, false, 1, two));
   }
   if (two) STL_RC(s.join(d.stream2, d.stream));  // results are read on d.stream
@@ -694,8 +699,9 @@ int drain(Device& d) {
   (void)hipSetDevice(d.ordinal);
   const hipError_t a = hipStreamSynchronize(d.copy);
   const hipError_t b = hipStreamSynchronize(d.stream);
-  const hipError_t c = d.stream2 ? hipStreamSynchronize(d.stream2) : hipSuccess;
-  return (a == hipSuccess && b == hipSuccess && c == hipSuccess) ? STL_OK : STL_EHIP;
+  const hipError_t c = hipStreamSynchronize(d.stream2);
+  const hipError_t e = d.stream3 ? hipStreamSynchronize(d.stream3) : hipSuccess;
+  return (a == hipSuccess && b == hipSuccess && c == hipSuccess && e == hipSuccess) ? STL_OK : STL_EHIP;
 }
 
 // Per-device copy: the shard's bitmap words to the host bitmap bytes
@@ -1169,7 +1175,7 @@ int verify_detached_device(const uint8_t* sig, const uint8_t* m, unsigned long l
     uint64_t* meta = static_cast<uint64_t*>(d.off.p);
     STL_TRY(stl::launch_hram_var(static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.pk.p),
                                  static_cast<uint8_t*>(d.pre.p), meta, meta + 1, 1, static_cast<uint8_t*>(d.msg.p), s));
-    STL_RC(run_verify(d, d.host, s, static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
+    STL_RC(run_verify(d, s, static_cast<uint8_t*>(d.sig.p), static_cast<uint8_t*>(d.msg.p),
                       static_cast<uint8_t*>(d.pk.p), 1, static_cast<uint64_t*>(d.bitmap.p), STL_POLICY_SODIUM_1_0_18,
                       true, 1));
     STL_TRY(hipMemcpyAsync(&word, d.bitmap.p, 8, hipMemcpyDeviceToHost, s));
@@ -1202,7 +1208,7 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  return run_verify(*d, stream_ctx(*d, s), s, d_sig, d_msg, d_pk, n, d_bitmap_words, stl::kernel_mode(flags), false,
+  return run_verify(*d, s, d_sig, d_msg, d_pk, n, d_bitmap_words, stl::kernel_mode(flags), false,
                     g_tune_streams.load());
 }
 
@@ -1215,7 +1221,7 @@ int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const ui
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  return run_verify(*d, stream_ctx(*d, s), s, d_sig, d_k, d_pk, n, d_bitmap_words, stl::kernel_mode(flags), true,
+  return run_verify(*d, s, d_sig, d_k, d_pk, n, d_bitmap_words, stl::kernel_mode(flags), true,
                     g_tune_streams.load());
 }
 
@@ -1264,8 +1270,9 @@ int stl_ed25519_sign_batch_device(const uint8_t* d_seed, const uint8_t* d_msg, s
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
   StreamCtx& c = stream_ctx(*d, s);
-  STL_RC(c.ws[0].ensure(stl::verify_ws_bytes(d->grid)));
-  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws[0].p), grid_for(*d, n), s));
+  std::lock_guard<std::mutex> lk(c.mu);
+  STL_RC(c.ws.ensure(stl::verify_ws_bytes(d->grid)));
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws.p), grid_for(*d, n), s));
   return STL_OK;
 }
 
@@ -1279,8 +1286,9 @@ int stl_debug_sign_adversarial_device(const uint8_t* d_seed, const uint8_t* d_ms
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
   StreamCtx& c = stream_ctx(*d, s);
-  STL_RC(c.ws[0].ensure(stl::verify_ws_bytes(d->grid)));
-  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws[0].p), grid_for(*d, n), s,
+  std::lock_guard<std::mutex> lk(c.mu);
+  STL_RC(c.ws.ensure(stl::verify_ws_bytes(d->grid)));
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws.p), grid_for(*d, n), s,
                            d_cls, d_param, d_msg_out));
   return STL_OK;
 }

@@ -197,3 +197,54 @@ def test_tuning_rejects_bad_values(stl):
                      (stl.TUNE_STREAMS, 5), (stl.TUNE_CHUNK_LOG2, 15), (stl.TUNE_CHUNK_LOG2, 21), (99, 1)):
         assert lib.stl_debug_tuning(key, bad) == N.STL_EINVAL, (key, bad)
     assert stl.execution_settings()["streams"] in (1, 2, 3, 4)
+
+
+@pytest.mark.timeout(300)
+def test_overlap_survives_caller_streams(stl, torch_cuda):
+    """libstl's streams come from a fixed per-device pool made in
+    stl_init, so streams a caller creates afterwards (here: a host API call,
+    then two caller streams with work on them) cannot take the hardware queue
+    of the stream a device-resident call spreads its chunks onto.  A 1M launch
+    on the caller's stream must stay at least 2 % below the serial sum of its
+    kernels (phase clock: prep + main + fallback one after another)."""
+    torch = torch_cuda
+    n = 1 << 20
+    rng = np.random.default_rng(404)
+    seeds = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    pk, sig = stl.sign_batch_device(seeds, msgs)
+    h = [a[:70_000].cpu().numpy() for a in (sig, msgs, pk)]
+    assert stl.verify_batch(*h).all()  # the host API first
+    extra = [torch.cuda.Stream() for _ in range(2)]
+    for s in extra:
+        with torch.cuda.stream(s):
+            torch.ones(1 << 20, device="cuda").sum()
+    torch.cuda.synchronize()
+    old = _apply(stl, (1, 1, 2, 18))  # the default execution
+    words = torch.empty(n // 64, dtype=torch.int64, device="cuda")
+    try:
+        def launches(k):
+            stream = torch.cuda.current_stream()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)]
+            ev[0].record(stream)
+            for i in range(k):
+                stl.verify_batch_device(sig, msgs, pk, out_words=words, stream=stream)
+                ev[i + 1].record(stream)
+            torch.cuda.synchronize()
+            return [ev[i].elapsed_time(ev[i + 1]) for i in range(k)]
+
+        launches(3)
+        overlapped = float(np.median(launches(10)))
+        assert stl.words_to_bool(words, n).all()
+        stl.reset_stats()
+        stl.set_phase_timing(True)
+        try:
+            launches(10)
+            st = stl.get_stats()
+        finally:
+            stl.set_phase_timing(False)
+        serial = sum(st["phase_ns"].values()) / max(1, st["phase_chunks"]) / 1e6
+        print(f"launch {overlapped:.3f} ms, serial kernel sum {serial:.3f} ms")
+        assert overlapped <= 0.98 * serial, (overlapped, serial)
+    finally:
+        _apply(stl, old)

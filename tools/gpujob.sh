@@ -7,6 +7,7 @@
 # gpurun_out/OUT and has its own time limit; the job stops at the first
 # failing step (no retries).  Steps:
 #   suite              pytest -m gpu (the round-end suite)
+#   tests:F1,F2        pytest -m gpu on the named test files / node ids only
 #   smoke              __graft_entry__.smoke()
 #   bench              python bench.py (defaults: the driver's N = 1 line)
 #   bench2             bench.py --gpus 2 --gather gloo (multi-rank rehearsal on one GPU)
@@ -35,6 +36,9 @@ run() {  # run NAME SECONDS CMD...
 for step in "$@"; do
   case $step in
     suite) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit $? ;;
+    tests:*)
+      T=${step#tests:}
+      run pytest_gpu_part 900 python -u -m pytest ${T//,/ } -m gpu -x -v --timeout 300 --timeout-method thread || exit $? ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py || exit $? ;;
     bench2) run bench_n2_rehearsal 600 python -u bench.py --gpus 2 --gather gloo --no-cpu-baseline || exit $? ;;
