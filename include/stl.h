@@ -361,9 +361,7 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
  * gives the same accept bits.  Returns the previous value, or STL_EINVAL for
  * an unknown key or a value out of range; value -1 only reads the setting.
  * Takes effect for launches made after the call. */
-#define STL_TUNE_FUSED_PREP 0 /* 1 (default): phase 1 (SHA-512, lattice, decodings) as one kernel; 0: two;
-                                 2: phase 1 inside the main kernel, per 64-signature unit (no phase-1
-                                 state in memory, one kernel boundary) */
+#define STL_TUNE_FUSED_PREP 0 /* 1 (default): phase 1 (SHA-512, lattice, decodings) as one kernel; 0: two */
 #define STL_TUNE_MAIN_QUEUE 1 /* 1 (default): the main kernel's waves pull 64-signature units from a
                                  counter; 0: static grid stride */
 #define STL_TUNE_STREAMS 2    /* 1..4: a device-resident verify call runs its chunks on this many

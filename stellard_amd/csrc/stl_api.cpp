@@ -982,7 +982,7 @@ int stl_debug_tuning(int key, int value) {
   }
   switch (key) {
     case STL_TUNE_FUSED_PREP:
-      if (value < 0 || value > 2) return STL_EINVAL;
+      if (value < 0 || value > 1) return STL_EINVAL;
       return g_tune_fused.exchange(value);
     case STL_TUNE_MAIN_QUEUE:
       if (value != 0 && value != 1) return STL_EINVAL;

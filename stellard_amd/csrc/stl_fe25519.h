@@ -37,7 +37,7 @@
 // Scheduling fence after each field multiply: keeps the pre-RA scheduler from
 // software-pipelining consecutive products (which multiplies live registers
 // and forced spills at 2-4 waves/SIMD).  Device-only hint; no-op on the host.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(STL_NO_FE_FENCE)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define STL_FE_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define STL_FE_FENCE()
@@ -150,7 +150,7 @@ STL_HD void fe_cmov(fe& h, const fe& a, const fe& b, bool c) {
 // Measured on MI355X (tools/microbench/isarate.hip, SIMD cycles per product
 // at 2 waves/SIMD): the compiler-scheduled fold 580 (mul) / 457 (sq); this
 // schedule 569 / 442 alone and 545 / 408 per product when two are paired.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(STL_NO_ACC_FENCE)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define STL_ACC_FENCE(acc) asm volatile("" : "+v"(acc))
 #else
 #define STL_ACC_FENCE(acc)

@@ -29,12 +29,7 @@ STL_HD void ge_cached_0(ge_cached& h) { fe_1(h.YpX); fe_1(h.YmX); fe_1(h.Z); fe_
 // T [1]: X*T <= 3, Y*Z <= 6, Z*T <= 3, X*Y <= 6 (fe_mul needs <= 7).
 STL_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
   fe X, Y, Z;
-#if STL_GE_NOPS == 2
-  fe_mul2(X, p.X, p.T, Y, p.Y, p.Z);
-  fe_mul(Z, p.Z, p.T);
-#else
   fe_mul3(X, p.X, p.T, Y, p.Y, p.Z, Z, p.Z, p.T);
-#endif
   r.X = X;
   r.Y = Y;
   r.Z = Z;
@@ -42,12 +37,7 @@ STL_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
 
 STL_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
   fe X, Y, Z, T;
-#if STL_GE_NOPS == 2
-  fe_mul2(X, p.X, p.T, Y, p.Y, p.Z);
-  fe_mul2(Z, p.Z, p.T, T, p.X, p.Y);
-#else
   fe_mul4(X, p.X, p.T, Y, p.Y, p.Z, Z, p.Z, p.T, T, p.X, p.Y);
-#endif
   r.X = X;
   r.Y = Y;
   r.Z = Z;
@@ -74,12 +64,7 @@ template <bool TO_P2 = false>
 STL_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe XX, YY, ZZ2, A, XpY;
   fe_add(XpY, p.X, p.Y);     // [2]
-#if STL_GE_NOPS == 2
-  fe_sq2(XX, p.X, YY, p.Y);
-  fe_sq2(ZZ2, p.Z, A, XpY);  // A [1]  (2^2 <= 7)
-#else
   fe_sq4(XX, p.X, YY, p.Y, ZZ2, p.Z, A, XpY);  // A [1]  (2^2 <= 7)
-#endif
   fe_add(ZZ2, ZZ2, ZZ2);     // [2]
   fe_add(r.Y, YY, XX);       // [2]
   fe_sub_nc<2>(r.Z, YY, XX); // [3]
@@ -117,12 +102,7 @@ STL_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe A, B, C, D, t, t2;
   fe_sub_nc<2>(t, p.Y, p.X); // [3]
   fe_add(t2, p.Y, p.X);      // [2]
-#if STL_GE_NOPS == 2
-  fe_mul2(A, t, q.YmX, B, t2, q.YpX);  // 3*1, 2*1
-  fe_mul2(C, q.T2d, p.T, D, p.Z, q.Z); // 2*1, 1*1
-#else
   fe_mul4(A, t, q.YmX, B, t2, q.YpX, C, q.T2d, p.T, D, p.Z, q.Z);  // 3*1, 2*1, 2*1, 1*1
-#endif
   fe_add(D, D, D);           // [2]
   fe_sub_nc<2>(r.X, B, A);   // [3]
   fe_add(r.Y, B, A);         // [2]
@@ -136,12 +116,7 @@ STL_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
   fe A, B, C, D, t, t2;
   fe_sub_nc<2>(t, p.Y, p.X); // [3]
   fe_add(t2, p.Y, p.X);      // [2]
-#if STL_GE_NOPS == 2
-  fe_mul2(A, t, q.ymx, B, t2, q.ypx);
-  fe_mul(C, q.xy2d, p.T);
-#else
   fe_mul3(A, t, q.ymx, B, t2, q.ypx, C, q.xy2d, p.T);
-#endif
   fe_add(D, p.Z, p.Z);       // [2]
   fe_sub_nc<2>(r.X, B, A);   // [3]
   fe_add(r.Y, B, A);         // [2]
@@ -206,93 +181,6 @@ STL_HD bool ge_frombytes_negate_vartime(ge_p3& h, const uint32_t s[8]) {
   fe_cmov(h.X, h.X, nx, fe_isnegative(h.X) == sign);
   fe_mul(h.T, h.X, h.Y);
   return m_ok || p_ok;
-}
-
-// Two decodings at once (A and R of one signature), every field product
-// paired with its twin (fe_sq2 / fe_mul2): the same results as two calls of
-// ge_frombytes_negate_vartime, with twice the independent mad chains per wave.
-STL_HD void fe_sqn2(fe& h0, const fe& x0, fe& h1, const fe& x1, int n) {
-  fe_sq2(h0, x0, h1, x1);
-#pragma unroll 1
-  for (int i = 1; i < n; ++i) fe_sq2(h0, h0, h1, h1);
-}
-
-STL_HD void fe_pow22523_2(fe& o0, const fe& z0, fe& o1, const fe& z1) {
-  fe a0, a1, b0, b1, c0, c1;
-  fe_sq2(a0, z0, a1, z1);
-  fe_sq2(b0, a0, b1, a1);
-  fe_sq2(b0, b0, b1, b1);                 // z^8
-  fe_mul2(b0, z0, b0, b1, z1, b1);        // z^9
-  fe_mul2(a0, a0, b0, a1, a1, b1);        // z^11
-  fe_sq2(a0, a0, a1, a1);                 // z^22
-  fe_mul2(a0, b0, a0, a1, b1, a1);        // z^(2^5-1)
-  fe_sqn2(b0, a0, b1, a1, 5);
-  fe_mul2(a0, b0, a0, a1, b1, a1);        // z^(2^10-1)
-  fe_sqn2(b0, a0, b1, a1, 10);
-  fe_mul2(b0, b0, a0, b1, b1, a1);        // z^(2^20-1)
-  fe_sqn2(c0, b0, c1, b1, 20);
-  fe_mul2(b0, c0, b0, b1, c1, b1);        // z^(2^40-1)
-  fe_sqn2(b0, b0, b1, b1, 10);
-  fe_mul2(a0, b0, a0, a1, b1, a1);        // z^(2^50-1)
-  fe_sqn2(b0, a0, b1, a1, 50);
-  fe_mul2(b0, b0, a0, b1, b1, a1);        // z^(2^100-1)
-  fe_sqn2(c0, b0, c1, b1, 100);
-  fe_mul2(b0, c0, b0, b1, c1, b1);        // z^(2^200-1)
-  fe_sqn2(b0, b0, b1, b1, 50);
-  fe_mul2(a0, b0, a0, a1, b1, a1);        // z^(2^250-1)
-  fe_sqn2(a0, a0, a1, a1, 2);
-  fe_mul2(o0, a0, z0, o1, a1, z1);        // z^(2^252-3)
-}
-
-STL_HD void ge_frombytes_negate_vartime2(ge_p3& h0, bool& ok0, const uint32_t s0[8], ge_p3& h1, bool& ok1,
-                                         const uint32_t s1[8]) {
-  fe u0, u1, v0, v1, w0, w1, x0, x1, one, d;
-  fe_frombytes(h0.Y, s0);
-  fe_frombytes(h1.Y, s1);
-  fe_1(h0.Z);
-  fe_1(h1.Z);
-  fe_1(one);
-  fe_const_d(d);
-  fe_sq2(u0, h0.Y, u1, h1.Y);
-  fe_mul2(v0, u0, d, v1, u1, d);
-  fe_sub(u0, u0, one);                    // u = y^2 - 1
-  fe_sub(u1, u1, one);
-  fe_add(v0, v0, one);                    // v = d y^2 + 1
-  fe_add(v1, v1, one);
-  fe_sq2(w0, v0, w1, v1);
-  fe_mul2(w0, w0, v0, w1, w1, v1);        // v^3
-  fe_sq2(x0, w0, x1, w1);
-  fe_mul2(x0, x0, v0, x1, x1, v1);
-  fe_mul2(x0, x0, u0, x1, x1, u1);        // u v^7
-  fe_pow22523_2(x0, x0, x1, x1);
-  fe_mul2(x0, x0, w0, x1, x1, w1);
-  fe_mul2(x0, x0, u0, x1, x1, u1);        // x = u v^3 (u v^7)^((p-5)/8)
-  fe vxx0, vxx1, chk;
-  fe_sq2(vxx0, x0, vxx1, x1);
-  fe_mul2(vxx0, vxx0, v0, vxx1, vxx1, v1);
-  fe_sub(chk, vxx0, u0);
-  const bool m0 = fe_iszero(chk);
-  fe_add(chk, vxx0, u0);
-  fe_carry(chk);
-  const bool p0 = fe_iszero(chk);
-  fe_sub(chk, vxx1, u1);
-  const bool m1 = fe_iszero(chk);
-  fe_add(chk, vxx1, u1);
-  fe_carry(chk);
-  const bool p1 = fe_iszero(chk);
-  fe sqm1, xs0, xs1;
-  fe_const_sqrtm1(sqm1);
-  fe_mul2(xs0, x0, sqm1, xs1, x1, sqm1);
-  fe_cmov(x0, x0, xs0, !m0);
-  fe_cmov(x1, x1, xs1, !m1);
-  fe nx;
-  fe_neg(nx, x0);
-  fe_cmov(h0.X, x0, nx, fe_isnegative(x0) == (s0[7] >> 31));
-  fe_neg(nx, x1);
-  fe_cmov(h1.X, x1, nx, fe_isnegative(x1) == (s1[7] >> 31));
-  fe_mul2(h0.T, h0.X, h0.Y, h1.T, h1.X, h1.Y);
-  ok0 = m0 || p0;
-  ok1 = m1 || p1;
 }
 
 // ge25519_tobytes: canonical y with the sign of x in bit 255.

@@ -9,11 +9,7 @@ namespace stl {
 constexpr uint32_t kBlock = 256;          // threads per workgroup (4 waves)
 // per-lane slot: two split tables (stl_kernels.hip lane_tables): 2 x 8 heads
 // of 8 quads (entry 0, the identity, shares one line) + 2 x 9 tail quads
-#ifdef STL_EXP_TABLE_ENTRIES  // timing experiment only: fewer stored multiples (wrong results)
-constexpr uint32_t kHeadQuads = 2 * STL_EXP_TABLE_ENTRIES * 8;
-#else
 constexpr uint32_t kHeadQuads = 2 * 8 * 8;
-#endif
 constexpr uint32_t kSlotQuads = kHeadQuads + 2 * 9;
 // workspace bytes per resident workgroup: 256 lanes x 146 x 16 B = 584 KiB
 constexpr size_t kWsBytesPerBlock = (size_t)kBlock * kSlotQuads * 16;
@@ -90,8 +86,7 @@ struct VerifyExec {
   const uint4* wide = nullptr;          // wide base tables
   unsigned long long* counters = nullptr;
   const PhaseClock* clock = nullptr;
-  int fused_prep = 1;                   // 0: scalar and point kernels; 1: phase 1 in one kernel;
-                                        // 2: phase 1 inside the main kernel (verify_whole_kernel)
+  int fused_prep = 1;                   // 0: scalar and point kernels; 1: phase 1 in one kernel
   bool main_queue = true;               // main kernel pulls 64-signature units from a counter
   bool concurrent = false;              // other chunks share the chip (host API, two streams): no
                                         // two-role phase 1 above pair_max (it trades work for latency)

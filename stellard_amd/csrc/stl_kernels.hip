@@ -32,11 +32,7 @@
 #define STL_VERIFY_WAVES_PER_SIMD 2
 #endif
 #ifndef STL_PRE_WAVES_PER_SIMD
-#ifdef STL_POINT_PAIRED
-#define STL_PRE_WAVES_PER_SIMD 2
-#else
 #define STL_PRE_WAVES_PER_SIMD 4
-#endif
 #endif
 // Scalar half of phase 1 (SHA-512 of k, lattice reduction): serial
 // dependency chains with few live registers, so occupancy hides latency.
@@ -77,26 +73,16 @@ __device__ __forceinline__ void stage_base_table(uint32_t* sB, int tables) {
 // lane, in whole aligned lines from the start of the area, then the 16-B
 // tails, 2 x 9 quads per lane (the main kernel keeps its tails in LDS).  Entry
 // 0 is the identity; its head is kIdentityHead, shared by every lane.
-// Not const: a const __device__ array lives in the constant address space, and
-// TableView::head's select between it and the global workspace then became a
-// generic pointer, so every table read was a flat load (STL_ID_CONST: A/B).
-#ifdef STL_ID_CONST
-__device__ __attribute__((aligned(128))) const uint4 kIdentityHead[8] = {
-#else
+// Not const: a const __device__ array lives in the constant address space,
+// and TableView::head's select between it and the global workspace then
+// becomes a generic pointer (flat loads); as a global array the table reads
+// are global loads (measured neutral, round 4).
 __device__ __attribute__((aligned(128))) uint4 kIdentityHead[8] = {
-#endif
     {1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 1u, 0u, 0u}, {0u, 0u, 0u, 0u},
     {0u, 0u, 1u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};  // YpX = YmX = Z = 1, T2d = 0
 __device__ __forceinline__ void lane_tables(uint4* ws, TableView& t1, TableView& t2) {
   const size_t lanes = (size_t)gridDim.x * kBlock;
-#ifdef STL_EXP_HALF_FOOTPRINT
-#warning "STL_EXP_HALF_FOOTPRINT is a timing experiment: verification results are wrong"
-  // timing experiment only (lanes 2i, 2i+1 share a slot: wrong results): the
-  // per-lane tables' footprint halved, below the 256 MB Infinity Cache
-  const size_t gl = ((size_t)blockIdx.x * kBlock + threadIdx.x) >> 1;
-#else
   const size_t gl = (size_t)blockIdx.x * kBlock + threadIdx.x;
-#endif
   uint4* head = ws + gl * kHeadQuads;
   uint4* tails = ws + lanes * kHeadQuads + gl * (2 * 9);
   t1 = TableView::split(head, tails, kIdentityHead);
@@ -104,25 +90,14 @@ __device__ __forceinline__ void lane_tables(uint4* ws, TableView& t1, TableView&
 }
 static_assert(kSlotQuads >= kHeadQuads + 2 * 9, "per-lane slot = heads + tails");
 
-// Phase-1 state (HalfState) is written once and read once: with STL_NT_STATE
-// it moves with non-temporal loads / stores so it does not displace the
-// per-lane tables in the Infinity Cache.
+// Phase-1 state (HalfState) is written once and read once (non-temporal
+// loads / stores measured +0.9 %, DESIGN_EXPERIMENTS.md).
 typedef unsigned int stl_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_state(uint4* p, uint4 v) {
-#ifdef STL_NT_STATE
-  stl_u32x4 x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, reinterpret_cast<stl_u32x4*>(p));
-#else
   *p = v;
-#endif
 }
 __device__ __forceinline__ uint4 ld_state(const uint4* p) {
-#ifdef STL_NT_STATE
-  const stl_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const stl_u32x4*>(p));
-  return make_uint4(x.x, x.y, x.z, x.w);
-#else
   return *p;
-#endif
 }
 
 template <int NQ, typename T>
@@ -275,11 +250,7 @@ __global__ __launch_bounds__(kBlock, STL_PRE_WAVES_PER_SIMD) void verify_prep_ke
 // quad_perm [1,0,3,2] (dpp_ctrl 0xB1), a register-to-register swap inside the
 // VALU -- __shfl_xor lowers to ds_bpermute_b32, an LDS round trip per value.
 __device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
-#ifdef STL_PAIR_SHFL  // A/B only: the LDS permute the pair kernels used before
-  return (uint32_t)__shfl_xor((int)v, 1);
-#else
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-#endif
 }
 
 
@@ -592,73 +563,21 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
 }
 
-// Wide-table rows in HBM: 7 quads (3 x 9 canonical limbs + a pad word), or,
-// with STL_WIDE_PACKED, 6 quads (3 x 8 words: the canonical values packed
-// like fe_tobytes) -- a 12 KiB LDS stage per wave instead of 14, so three
-// 256-thread workgroups fit in a CU's 160 KiB; unpacked with fe_frombytes.
-#ifdef STL_WIDE_PACKED
-constexpr int kWideQuads = 6;
-#else
+// Wide-table rows in HBM: 7 quads (3 x 9 canonical limbs + a pad word).
 constexpr int kWideQuads = 7;
-#endif
 
 __device__ __forceinline__ void wide_row_to_niels(ge_niels& n, const uint32_t* row) {
-#ifdef STL_WIDE_PACKED
-  fe_frombytes(n.ypx, row);
-  fe_frombytes(n.ymx, row + 8);
-  fe_frombytes(n.xy2d, row + 16);
-#else
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     n.ypx.v[i] = row[i];
     n.ymx.v[i] = row[9 + i];
     n.xy2d.v[i] = row[18 + i];
   }
-#endif
 }
 
-// Wide-table reader of the main kernel: each lane's two rows go straight from
-// L2 / the Infinity Cache into its wave's LDS stage by global_load_lds, issued
-// before the position's doublings -- the latency is hidden and no VGPRs are
-// held across the doublings.  Stage layout [row][chunk][lane]: conflict-free
-// reads.
-struct WideLds {
-  const uint4* gtab;  // 2 * kWideEntries rows of kWideQuads uint4
-  uint4* stage;       // this wave's 2 * kWideQuads * 64 uint4
-  uint32_t lane;
-  int d[2];
-  __device__ void prefetch(int d0, int d1) {
-    d[0] = d0;
-    d[1] = d1;
-#pragma unroll
-    for (int w = 0; w < 2; ++w) {
-      const uint32_t a = (uint32_t)(d[w] < 0 ? -d[w] : d[w]);
-      const uint4* src = gtab + ((size_t)w * kWideEntries + a) * kWideQuads;
-#pragma unroll
-      for (int c = 0; c < kWideQuads; ++c)
-        __builtin_amdgcn_global_load_lds(src + c,
-                                         (__attribute__((address_space(3))) void*)(stage + (w * kWideQuads + c) * 64),
-                                         16, 0, 0);
-    }
-  }
-  __device__ void madd(ge_p1p1& t, const ge_p3& acc, int which) const {
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the rows have landed in LDS
-    uint32_t row[4 * kWideQuads];
-#pragma unroll
-    for (int c = 0; c < kWideQuads; ++c) {
-      const uint4 v = stage[(which * kWideQuads + c) * 64 + lane];
-      row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
-    }
-    ge_niels n;
-    wide_row_to_niels(n, row);
-    ge_niels_cneg(n, d[which] < 0);
-    ge_madd(t, acc, n);
-  }
-};
-
-// Wide rows read straight into VGPRs at the madd (the default, since the
-// per-lane table tails take the LDS; with STL_TAILS_GLOBAL the rows are staged
-// in LDS by WideLds instead).
+// Wide rows read straight into VGPRs at the madd (the per-lane table tails
+// take the LDS; staging the rows in LDS by global_load_lds measured slower,
+// DESIGN_EXPERIMENTS.md).
 struct WideGlobal {
   const uint4* gtab;
   int d[2];
@@ -690,22 +609,16 @@ struct WideGlobal {
 // and the kernel's last round is not fixed in advance; without it the units
 // are dealt out statically (grid stride).  Every wave leaves after one pull
 // past the end.
-#ifdef STL_MAIN_NUM_VGPR
-#define STL_MAIN_ATTR __attribute__((amdgpu_num_vgpr(STL_MAIN_NUM_VGPR)))
-#else
-#define STL_MAIN_ATTR
-#endif
 // JOINT (chunks without key dedup): one joint radix-4 table of a*P1 + b*P2
 // per lane (verify_phase2_joint); otherwise two radix-16 tables, the A-table
 // possibly the key's shared one (verify_phase2_half).
 template <bool JOINT>
-__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_kernel(
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint64_t* __restrict__ bitmap,
     uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
     const uint4* __restrict__ keytabs, const uint4* __restrict__ widetabs, uint32_t* __restrict__ queue) {
   TableView tab1, tab2;
   lane_tables(ws, tab1, tab2);
-#ifndef STL_TAILS_GLOBAL
   // The tables' 16-B tails live in LDS, [table*9 + entry][lane] (conflict-
   // free; 72 KiB per workgroup, two workgroups per CU): a lookup reads one
   // aligned HBM line (its head) and one LDS quad.  LDS then has no room for
@@ -715,15 +628,8 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
   tab1.tail = &tails[0][threadIdx.x];
   tab2.tail = &tails[9][threadIdx.x];
   tab1.tstride = tab2.tstride = kBlock;
-#endif
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-#if defined(STL_WIDE_GLOBAL) || !defined(STL_TAILS_GLOBAL)
   WideGlobal wl{wide, {0, 0}};
-  (void)lane;
-#else
-  __shared__ uint4 wstage[kBlock / 64][2 * kWideQuads * 64];
-  WideLds wl{wide, wstage[wave], lane, {0, 0}};
-#endif
   const uint32_t units = (cnt + 63) >> 6;
   const uint32_t stride = gridDim.x * (kBlock / 64);
   uint32_t unit = blockIdx.x * (kBlock / 64) + wave;
@@ -755,80 +661,13 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR vo
   }
 }
 
-// Phase 1 and phase 2 in one kernel (STL_TUNE_FUSED_PREP 2): a wave takes a
-// 64-signature unit and runs verify_prep_kernel's work on it (k, half-size
-// scalars, pre-checks, decodings) and then the Straus loop, with the phase-1
-// state in registers -- no 224-B HalfState write and read per signature and
-// one kernel boundary per chunk.  The decodings run at the main kernel's
-// occupancy (2 waves/SIMD, no spills) instead of 4 waves with spills.  The
-// fallback flags go to fb_words for verify_fallback_kernel, as phase 1's do.
-template <bool PRE_K>
-__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_whole_kernel(
-    const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
-    uint32_t base, uint32_t cnt, uint32_t policy, uint64_t* __restrict__ fb_words, uint64_t* __restrict__ bitmap,
-    uint4* __restrict__ ws, const uint4* __restrict__ wide, unsigned long long* __restrict__ ctr,
-    uint32_t* __restrict__ queue) {
-  TableView tab1, tab2;
-  lane_tables(ws, tab1, tab2);
-  __shared__ uint4 tails[18][kBlock];
-  tab1.tail = &tails[0][threadIdx.x];
-  tab2.tail = &tails[9][threadIdx.x];
-  tab1.tstride = tab2.tstride = kBlock;
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  WideGlobal wl{wide, {0, 0}};
-  const uint32_t units = (cnt + 63) >> 6;
-  const uint32_t stride = gridDim.x * (kBlock / 64);
-  uint32_t unit = blockIdx.x * (kBlock / 64) + wave;
-  for (;;) {
-    if (queue) {  // wave-uniform: one atomic per wave and unit
-      uint32_t u = 0;
-      if (lane == 0) u = atomicAdd(queue, 1u);
-      unit = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
-    }
-    if (unit >= units) break;
-    const uint32_t wbase = unit * 64;
-    const uint32_t t = wbase + lane;
-    const bool live = t < cnt;
-    const size_t j = (size_t)base + (live ? t : cnt - 1);
-    HalfState h;
-    {
-      uint32_t R[8], S[8], A[8], k[8];
-      ld8(R, sig + 64 * j);
-      ld8(S, sig + 64 * j + 32);
-      ld8(A, pk + 32 * j);
-      load_k(k, R, A, msg_or_k, j, PRE_K);
-      verify_phase1_scalars(h, S, k);
-#ifdef STL_WHOLE_PAIRED  // the two square-root chains interleaved (more ILP, more registers)
-      const uint32_t pol = core_policy(policy);
-      const bool pre_ok = verify_prechecks(R, S, A, pol) && composite_s_ok(S, pol) && r_is_canonical(R);
-      ge_p3 negA, negQ;
-      bool okA, okR;
-      ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
-      finish_phase1_points(h, negA.X, negA.Y, negQ.X, negQ.Y, pre_ok && okA && okR);
-#else
-      verify_phase1_points(h, R, S, A, core_policy(policy));
-#endif
-    }
-    if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
-    const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
-    const bool ok = verify_phase2_half(h, tab1, tab2, wl) && live;
-    const uint64_t word = __ballot(ok);
-    if (lane == 0) {
-      fb_words[wbase >> 6] = fb;
-      bitmap[(base + wbase) >> 6] = word;
-      if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popcll(word));  // accepted (stl_get_stats)
-    }
-    if (!queue) unit += stride;
-  }
-}
-
 // Phase 2 for small batches (2 x cnt lanes fit in one round of resident
 // lanes, no key dedup): lanes 2j and 2j+1 run signature j's two half chains
 // (verify_phase2_pair_chain) on one table each, swap their sums across the
 // pair, and both test that they cancel.  A wave decides 32 signatures: the
 // even bits of its ballot are one 32-bit half of a bitmap word (the other
 // half is the next wave's, in the same tile).
-__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) STL_MAIN_ATTR void verify_main_pair_kernel(
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_pair_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint32_t policy, uint64_t* __restrict__ bitmap,
     uint64_t* __restrict__ fb_words, uint4* __restrict__ ws, const uint4* __restrict__ wide,
     unsigned long long* __restrict__ ctr) {
@@ -1287,19 +1126,7 @@ __global__ __launch_bounds__(kBlock) void wide_table_kernel(uint32_t* __restrict
   const int which = r >= kWideEntries ? 1 : 0;
   uint32_t row[28];
   wide_entry(row, which, r - (uint32_t)which * kWideEntries, &kBaseNiels[0][0][0]);
-#ifdef STL_WIDE_PACKED
-  uint32_t packed[24];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    fe f;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) f.v[i] = row[9 * k + i];
-    fe_tobytes(packed + 8 * k, f);  // canonical already: packs the 255 bits
-  }
-  const uint32_t* src = packed;
-#else
   const uint32_t* src = row;
-#endif
   uint4* q = reinterpret_cast<uint4*>(out) + (size_t)r * kWideQuads;
 #pragma unroll
   for (int c = 0; c < kWideQuads; ++c) q[c] = make_uint4(src[4 * c], src[4 * c + 1], src[4 * c + 2], src[4 * c + 3]);
@@ -1353,33 +1180,8 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     // duplicating work, so they pay up to twice that size (two pair waves per
     // SIMD; no workspace), ahead of the one-lane main kernel
     // (verify_finish_pair_kernel in between).
-#ifdef STL_POINT_PAIR_ALL
-    const bool pair_point = pair || ((policy & kModeOneLane) == 0 && !dedup);
-#else
     const bool pair_point = pair || (!x.concurrent && (policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
-#endif
     const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
-    if (x.fused_prep == 2 && !pair && !dedup) {
-      // the whole verification in one kernel (phase clock: all of it is "main")
-      mark(0);
-      mark(1);
-      mark(2);
-      if (pre_k)
-        hipLaunchKernelGGL(verify_whole_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                           policy, fb, bitmap, slots, wide, counters, qctr);
-      else
-        hipLaunchKernelGGL(verify_whole_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                           policy, fb, bitmap, slots, wide, counters, qctr);
-      mark(3);
-      if (pre_k)
-        hipLaunchKernelGGL(verify_fallback_kernel<true>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                           policy, fb, bitmap, slots, counters);
-      else
-        hipLaunchKernelGGL(verify_fallback_kernel<false>, g2, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt,
-                           policy, fb, bitmap, slots, counters);
-      mark(4);
-      return hipGetLastError();
-    }
     const bool fused = x.fused_prep != 0 && !pair_point && !dedup;
     mark(0);
     // pair_point implies !dedup or pair (pair chunks ignore STL_DEDUP_KEYS)
@@ -1434,11 +1236,9 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     if (pair)
       hipLaunchKernelGGL(verify_main_pair_kernel, gp, dim3(kBlock), 0, stream, pre, base, cnt, policy, bitmap, fb,
                          slots, wide, counters);
-#ifndef STL_NO_JOINT
     else if (!dedup)
       hipLaunchKernelGGL(verify_main_kernel<true>, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
                          counters, nullptr, nullptr, qctr);
-#endif
     else
       hipLaunchKernelGGL(verify_main_kernel<false>, g2, dim3(kBlock), 0, stream, pre, base, cnt, bitmap, slots, wide,
                          counters, dedup ? keytabs : nullptr, dedup ? widetabs : nullptr, qctr);

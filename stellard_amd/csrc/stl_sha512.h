@@ -84,9 +84,6 @@ STL_HD W64 shr(W64 x) {
 STL_HD W64 xor3(W64 a, W64 b, W64 c) { return W64{a.lo ^ b.lo ^ c.lo, a.hi ^ b.hi ^ c.hi}; }
 
 STL_HD W64 add(W64 a, W64 b) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(STL_SHA_ADD64)
-  return w64(u64(a) + u64(b));
-#endif
   unsigned c;
   const uint32_t lo = __builtin_addc(a.lo, b.lo, 0u, &c);
   const uint32_t hi = __builtin_addc(a.hi, b.hi, c, &c);
@@ -143,9 +140,6 @@ STL_HD void sha512_compress(uint64_t st[8], uint64_t w64in[16]) {
     const W64 S0 = xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a));
     const W64 t2 = add(S0, maj(a, b, c));
     h = g; g = f; f = e; e = add(d, t1); d = c; c = b; b = a; a = add(t1, t2);
-#ifdef STL_SHA_FENCE
-    STL_FE_FENCE();
-#endif
   }
   st[0] = u64(add(w64(st[0]), a)); st[1] = u64(add(w64(st[1]), b));
   st[2] = u64(add(w64(st[2]), c)); st[3] = u64(add(w64(st[3]), d));

@@ -191,12 +191,7 @@ STL_HD void build_cached_table(const TableView& tab, const ge_p3& P) {
   ge_p1p1_to_p3(p3, t);
   ge_p3_to_cached(c, p3);
   tab.store(2, c);
-#ifdef STL_EXP_TABLE_ENTRIES
-#warning "STL_EXP_TABLE_ENTRIES is a timing experiment: verification results are wrong"
-  constexpr int kLast = STL_EXP_TABLE_ENTRIES;
-#else
   constexpr int kLast = 8;
-#endif
 #pragma unroll 1
   for (int e = 3; e <= kLast; ++e) {
     ge_madd(t, p3, n1);
@@ -229,11 +224,7 @@ STL_HD void dbl4(ge_p3& acc, ge_p2& acc2) {
   ge_p1p1 t;
 #pragma unroll 1
   for (int r = 0; r < 3; ++r) {
-#ifdef STL_NO_LAZY_DBL
-    ge_p2_dbl(t, acc2);
-#else
     ge_p2_dbl<true>(t, acc2);
-#endif
     ge_p1p1_to_p2(acc2, t);
   }
   ge_p2_dbl(t, acc2);
@@ -440,14 +431,10 @@ STL_HD void verify_phase1_points(HalfState& o, const uint32_t R[8], const uint32
   ok = ok && composite_s_ok(S, policy) && r_is_canonical(R);  // before the decodings: R, S not live across them
   ge_p3 negA, negQ;
   bool okA, okR;
-#ifndef STL_POINT_PAIRED
   // one decoding at a time: 128 VGPRs, 4 waves/SIMD; measured 1-3 % faster
   // than the paired chains at 2 waves
   okA = ge_frombytes_negate_vartime(negA, A);
   okR = ge_frombytes_negate_vartime(negQ, R);
-#else
-  ge_frombytes_negate_vartime2(negA, okA, A, negQ, okR, R);
-#endif
   ok = ok && okA && okR;
   finish_phase1_points(o, negA.X, negA.Y, negQ.X, negQ.Y, ok);
 }
@@ -685,31 +672,14 @@ STL_HD bool verify_phase2_half(const HalfState& p, const TableView& tab1, const 
     // of independent work per wave): their latency (L2 / Infinity Cache) is
     // hidden instead of stalling the adds.
     ge_cached ca, cq;
-#if defined(STL_EXP_ENTRY0)
-#warning "STL_EXP_ENTRY0 is a timing experiment: verification results are wrong"
-    // timing experiment only (wrong results): every lookup reads entry 0 of
-    // its table (cache-resident) -- the memory-side cost of the lookups
-    if (cadd) t1.load(0, ca);
-    tab2.load(0, cq);
-#elif !defined(STL_NO_TABLE_PREFETCH)
     // Unconditional loads (entry 0 where a wide-key position skips the A-add):
     // a load under `if (cadd)` made the compiler merge its registers at the
     // end of the branch, i.e. wait for the load there -- before the doublings
     // it is meant to overlap.
-#if defined(STL_EXP_TABLE_ENTRIES)
-    t1.load(cadd ? min(dc < 0 ? -dc : dc, STL_EXP_TABLE_ENTRIES) : 0, ca);
-    tab2.load(min(dq < 0 ? -dq : dq, STL_EXP_TABLE_ENTRIES), cq);
-#else
     t1.load(cadd ? (dc < 0 ? -dc : dc) : 0, ca);
     tab2.load(dq < 0 ? -dq : dq, cq);
-#endif
-#endif
     if (bpos) wide.prefetch(de0, de1);
     if (i != npos - 1) dbl4(acc, acc2);
-#ifdef STL_NO_TABLE_PREFETCH
-    if (cadd) t1.load(dc < 0 ? -dc : dc, ca);
-    tab2.load(dq < 0 ? -dq : dq, cq);
-#endif
     if (cadd) {
       ge_cached_cneg(ca, (dc < 0) != a_flip);
       ge_add_cached(t, acc, ca);
