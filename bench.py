@@ -570,11 +570,17 @@ def gpu_run(args, world, rank, local):
                 td = json.load(f)
             traffic = (td.get("main_kernel") or {}).get("hbm_bytes_per_launch")
             traffic_build = provenance(td, tp)
-        valu_busy = None
+        valu_busy, issue = None, None
         vp = os.path.join(ROOT, "profiles", "valu_latest.json")
         if os.path.exists(vp):
             with open(vp) as f:
                 vd = json.load(f)
+            mk = next((v for k, v in vd.get("kernels", {}).items() if "verify_main_kernel" in k), {})
+            if mk.get("issue_bound_ms"):
+                issue = {"issue_bound_ms": mk["issue_bound_ms"], "frac_of_issue_bound": mk["issue_bound_ms"] / main_ms,
+                         "effective_clock_ghz": mk.get("effective_clock_ghz"),
+                         "model": mk.get("issue_bound_model"),
+                         "source": "profiles/valu_latest.json (main kernel PMC instruction counts)"}
             valu_busy = {"launch_pct": vd.get("launch_valu_busy_pct"),
                          "per_kernel_pct": {k: v.get("VALUBusy") for k, v in vd.get("kernels", {}).items()},
                          "source": vd.get("source", "rocprofv3 --pmc VALUBusy, profiles/valu_latest.json"),
@@ -601,6 +607,8 @@ def gpu_run(args, world, rank, local):
                        "execution": V.execution_settings()},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
+                         "algorithmic_bytes": BYTES_PER_VERIFY * n,
+                         "traffic_over_algorithmic": traffic / (BYTES_PER_VERIFY * n) if traffic else None,
                          "traffic_build": traffic_build, "sources_sha256": digest,
                          "kernel": "verify_main_kernel (dominant: %.0f %% of the launch)"
                                    % (100.0 * main_ms / max(1e-9, sum(phase_ms.values()))),
@@ -614,7 +622,8 @@ def gpu_run(args, world, rank, local):
                          "launch": "every kernel of one stl_ed25519_verify_batch_device call (phase 1, main, "
                                    "fallback), HIP events around each call of the timed region",
                          "hbm_frac": BYTES_PER_VERIFY * per_launch / (HBM_PEAK_GBS * 1e9),
-                         "valu_busy_pmc": valu_busy},
+                         "valu_busy_pmc": valu_busy,
+                         "issue_bound": issue},
             "cpu_baseline": None,
             "stats": {"source": "stl_get_stats over the timed launches (rank 0)",
                       "accepted": st["accepted"], "full_length_lanes": st["full_length_lanes"],

@@ -615,3 +615,28 @@ def test_bitmap_gatherv_one_rank(stl, torch_cuda):
     with pytest.raises(N.StlError) as e:  # no communicator
         stl.bitmap_gatherv_device(words, [0, 1000], full, root=0)
     assert e.value.rc == N.STL_ERCCL
+
+
+@pytest.mark.timeout(300)
+def test_multi_device_in_process_rccl_gather(stl, torch_cuda, oracle, golden):
+    """stellard's own shape -- one process, every visible
+    device (stl_init with all of them and STL_CFG_RCCL_GATHER: ncclCommInitAll,
+    ncclGather of equal index shards, grouped send / recv of byte-balanced
+    shards).  Index shards against the golden bits, byte shards (variable-length
+    preimages) against the oracle, both with and without the gather.  Needs
+    two or more GPUs; skips on a one-GPU box (the [rccl1] variants of the tests
+    above run the same code with one device)."""
+    from stellard_amd import _native as N
+    ndev = torch_cuda.cuda.device_count()
+    if ndev < 2:
+        pytest.skip(f"{ndev} GPU visible: the in-process multi-device gather needs >= 2")
+    sig, msg, pk, exp = _golden_rows(golden, 50_000 + 37, seed=99)
+    pres, psig, ppk = _preimage_corpus(oracle, 3_001, seed=98)
+    pexp = oracle.tx_verify_batch(pres, psig, ppk)
+    for flags in (N.STL_CFG_RCCL_GATHER, N.STL_CFG_NO_RCCL):
+        with reinit(stl, flags=flags):
+            assert N.load().stl_device_count() == ndev
+            if flags == N.STL_CFG_RCCL_GATHER:
+                assert stl.comm_info()[0] == ndev
+            assert np.array_equal(stl.verify_batch(sig, msg, pk), exp), flags
+            assert np.array_equal(stl.tx_verify_batch(pres, psig, ppk), pexp), flags
