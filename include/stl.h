@@ -77,6 +77,13 @@ extern "C" {
  * pairs (STL_ONE_LANE below) run on pairs instead: latency-bound there, the
  * pairs are faster. */
 #define STL_DEDUP_KEYS 0x8u
+/* The host batch calls (stl_ed25519_verify_batch, stl_tx_verify_batch, the
+ * blob calls) choose STL_DEDUP_KEYS by themselves for every 64K-row chunk in
+ * which a sample of 2,048 keys shows at least a quarter repeating (host-side,
+ * about 20 us per chunk); this flag turns the automatic choice off (A/B and
+ * callers that know their keys are distinct).  The device-resident calls
+ * never sample (the keys are in HBM): there the caller sets STL_DEDUP_KEYS. */
+#define STL_NO_AUTO_DEDUP 0x20u
 /* Small chunks run each signature on two lanes, which ends a launch that
  * cannot fill the device sooner: the main kernel up to
  * a quarter of the device's resident lanes (one pair wave per SIMD; 32,768
@@ -338,6 +345,9 @@ typedef struct stl_stats {
    * (Straus loop), [3] fallback -- and the number of chunks timed. */
   uint64_t phase_ns[4];
   uint64_t phase_chunks;
+  /* host batch chunks that chose STL_DEDUP_KEYS by themselves (STL_NO_AUTO_DEDUP
+   * above); a struct without this field (struct_size = its offset) is accepted */
+  uint64_t auto_dedup_chunks;
 } stl_stats;
 int stl_get_stats(stl_stats *out);
 void stl_reset_stats(void);

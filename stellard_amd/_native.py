@@ -32,6 +32,7 @@ STL_REQUIRE_S_LT_L = 0x2
 STL_FULL_LENGTH = 0x4
 STL_DEDUP_KEYS = 0x8
 STL_ONE_LANE = 0x10
+STL_NO_AUTO_DEDUP = 0x20
 STL_DEBUG_RAW_PREDICATE = 0x80000000  # test-only: no S < L (stl.h)
 
 # stl_debug_tuning keys

@@ -319,7 +319,8 @@ int g_pcomm_ranks = 0;
 unsigned long long* dev_counters(Device& d) { return static_cast<unsigned long long*>(d.counters.p); }
 
 // ---- host-side statistics (stl_get_stats) and tracing (STL_TRACE=1) ----
-std::atomic<uint64_t> g_st_batches{0}, g_st_sigs{0}, g_st_errors{0}, g_st_host_ns{0}, g_st_gather_ns{0};
+std::atomic<uint64_t> g_st_batches{0}, g_st_sigs{0}, g_st_errors{0}, g_st_host_ns{0}, g_st_gather_ns{0},
+    g_st_auto_dedup{0};
 bool g_trace = false;
 
 uint64_t now_ns() {
@@ -569,7 +570,49 @@ struct Batch {
   const uint32_t* len;
   uint8_t *bitmap, *status, *txid;
   uint32_t policy, kind;
+  bool auto_dedup;  // choose STL_DEDUP_KEYS per chunk from a key sample (keys_repeat)
 };
+
+// The signing key of host row i, for the automatic dedup choice only: the
+// pk array, or in a serialized object the 32 bytes after the first
+// SigningPubKey header (0x73, VL length 0x20) -- a wrong guess only picks the
+// slower path, never other bits.
+const uint8_t* row_key(const Batch& b, size_t i) {
+  if (b.mode != Mode::kBlob) return b.pk + 32 * i;
+  const uint8_t* p = b.bytes + b.off[i];
+  const size_t len = b.len[i], lim = len < 34 ? 0 : std::min<size_t>(len - 34, 256);
+  for (size_t j = 0; j + 1 <= lim; ++j)
+    if (p[j] == 0x73 && p[j + 1] == 0x20) return p + j + 2;
+  return nullptr;
+}
+
+// Host-side estimate of key repetition over rows [lo, hi) (a
+// ledger's signers repeat -- 1,000 accounts for 100k transactions): up to
+// 2,048 evenly spaced keys, 64-bit fingerprints in an open-addressing table;
+// true when at least a quarter of the sampled keys repeat an earlier one,
+// where decoding each key once pays (key dedup).  About
+// 20 us per 64K-row chunk on the host.
+bool keys_repeat(const Batch& b, size_t lo, size_t hi) {
+  constexpr size_t kSample = 2048, kSlots = 4096;
+  const size_t n = hi - lo;
+  if (n < 4 * 64) return false;
+  const size_t s = std::min(n, kSample);
+  uint64_t table[kSlots] = {};
+  size_t dups = 0;
+  for (size_t k = 0; k < s; ++k) {
+    const uint8_t* key = row_key(b, lo + k * n / s);
+    if (!key) continue;
+    uint64_t a, c;
+    std::memcpy(&a, key, 8);
+    std::memcpy(&c, key + 24, 8);
+    uint64_t f = (a ^ (c * 0x9E3779B97F4A7C15ull)) | 1u;  // 0 marks an empty slot
+    size_t h = (size_t)((f * 0xD6E8FEB86659FD93ull) >> 52) & (kSlots - 1);
+    while (table[h] && table[h] != f) h = (h + 1) & (kSlots - 1);
+    if (table[h] == f) ++dups;
+    table[h] = f;
+  }
+  return 4 * dups >= s;
+}
 
 // Host-side state of one shard; lives until the batch has synchronised (the
 // staging vectors are sources of asynchronous copies).
@@ -663,6 +706,25 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
   // One stream while the phase clock is on: its per-kernel times must not
   // overlap.
   const bool two = g_tune_streams.load() > 1 && n > kPipeChunk && !phase_clock(d);
+  // automatic key dedup: chunk c's policy from a sample of its keys; the
+  // dedup-sized workspaces are taken before the first chunk, so no workspace
+  // grows while earlier chunks still run on it
+  std::vector<uint32_t> cpol((n + kPipeChunk - 1) / kPipeChunk, b.policy);
+  if (b.auto_dedup) {
+    bool any = false;
+    for (size_t c = 0; c < cpol.size(); ++c)
+      if (keys_repeat(b, lo + c * kPipeChunk, lo + std::min(n, (c + 1) * kPipeChunk))) {
+        cpol[c] |= stl::kModeDedupKeys;
+        any = true;
+        g_st_auto_dedup++;
+      }
+    if (any)
+      for (hipStream_t ks : {d.stream, d.stream2}) {
+        StreamCtx& c = stream_ctx(d, ks);
+        std::lock_guard<std::mutex> lk(c.mu);
+        STL_RC(c.ws.ensure(stl::verify_ws_bytes(d.grid, true)));
+      }
+  }
   if (two && b.mode != Mode::kSig) STL_RC(d.ctr2.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
   for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
     const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
@@ -685,7 +747,7 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
                                   dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0, kctr,
                                   hash_grid(d), ks, b.kind));
     STL_RC(run_verify(d, ks, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
-                      static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, b.policy, false, 1, two));
+                      static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, cpol[c0 / kPipeChunk], false, 1, two));
   }
   if (two) STL_RC(s.join(d.stream2, d.stream));  // results are read on d.stream
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
@@ -771,9 +833,15 @@ int gather_to_host(const Batch& b, std::vector<Shard>& sh, size_t n, size_t per,
 
 int check_flags(uint32_t flags) {
   return (flags & ~(STL_POLICY_MASK | STL_REQUIRE_S_LT_L | STL_FULL_LENGTH | STL_DEDUP_KEYS | STL_ONE_LANE |
-                    STL_DEBUG_RAW_PREDICATE))
+                    STL_NO_AUTO_DEDUP | STL_DEBUG_RAW_PREDICATE))
              ? STL_EINVAL
              : STL_OK;
+}
+
+// Host batches choose key dedup per chunk unless the caller decided
+// (STL_DEDUP_KEYS on, STL_NO_AUTO_DEDUP off) or the chunk runs on lane pairs.
+bool auto_dedup(uint32_t flags) {
+  return (flags & (STL_DEDUP_KEYS | STL_NO_AUTO_DEDUP | STL_FULL_LENGTH)) == 0;
 }
 
 int run_batch(const Batch& b, size_t n, uint64_t* gather_ns) {
@@ -1002,7 +1070,9 @@ int stl_debug_tuning(int key, int value) {
 }
 
 int stl_get_stats(stl_stats* out) {
-  if (!out || out->struct_size != sizeof(stl_stats)) return STL_EINVAL;
+  if (!out || (out->struct_size != sizeof(stl_stats) && out->struct_size != offsetof(stl_stats, auto_dedup_chunks)))
+    return STL_EINVAL;
+  if (out->struct_size == sizeof(stl_stats)) out->auto_dedup_chunks = g_st_auto_dedup.load();
   out->batches = g_st_batches.load();
   out->signatures = g_st_sigs.load();
   out->errors = g_st_errors.load();
@@ -1036,6 +1106,7 @@ void stl_reset_stats(void) {
   g_st_errors = 0;
   g_st_host_ns = 0;
   g_st_gather_ns = 0;
+  g_st_auto_dedup = 0;
   DeviceGuard guard;
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& d : g_devs)
@@ -1075,7 +1146,7 @@ int stl_ed25519_verify_batch(const uint8_t* sig, const uint8_t* msg, const uint8
   if (!sig || !msg || !pk || !accept_bitmap) return STL_EINVAL;
   STL_RC(check_flags(flags));
   const Batch b{Mode::kSig, sig, msg, pk, nullptr, nullptr, nullptr, accept_bitmap, nullptr, nullptr,
-                stl::kernel_mode(flags), 0u};
+                stl::kernel_mode(flags), 0u, auto_dedup(flags)};
   CallSpan span{"stl_ed25519_verify_batch", n};
   uint64_t g = 0;
   const int rc = run_batch(b, n, &g);
@@ -1088,7 +1159,7 @@ int stl_tx_verify_batch(const uint8_t* preimages, const uint64_t* offset, const 
   if (!preimages || !offset || !len || !sig || !pk || !accept_bitmap) return STL_EINVAL;
   STL_RC(check_flags(flags));
   const Batch b{Mode::kPre, sig, nullptr, pk, preimages, offset, len, accept_bitmap, nullptr, nullptr,
-                stl::kernel_mode(flags), 0u};
+                stl::kernel_mode(flags), 0u, auto_dedup(flags)};
   CallSpan span{"stl_tx_verify_batch", n};
   uint64_t g = 0;
   const int rc = run_batch(b, n, &g);
@@ -1102,7 +1173,7 @@ int stl_signed_blob_verify_batch(uint32_t kind, const uint8_t* blobs, const uint
   if (!blobs || !offset || !len || !accept_bitmap) return STL_EINVAL;
   STL_RC(check_flags(flags));
   const Batch b{Mode::kBlob, nullptr, nullptr, nullptr, blobs, offset, len, accept_bitmap, status, id,
-                stl::kernel_mode(flags), kind};
+                stl::kernel_mode(flags), kind, auto_dedup(flags)};
   CallSpan span{kind == STL_BLOB_VALIDATION ? "stl_signed_blob_verify_batch(validation)" : "stl_tx_blob_verify_batch",
                 n};
   uint64_t g = 0;

@@ -26,6 +26,7 @@ FULL_LENGTH = N.STL_FULL_LENGTH
 # OR into `policy` to decode each distinct public key of a batch once
 DEDUP_KEYS = N.STL_DEDUP_KEYS
 ONE_LANE = N.STL_ONE_LANE
+NO_AUTO_DEDUP = N.STL_NO_AUTO_DEDUP
 
 
 class BadInputs(RuntimeError):
@@ -476,7 +477,8 @@ class Stats(ctypes.Structure):
                 ("batches", ctypes.c_uint64), ("signatures", ctypes.c_uint64), ("errors", ctypes.c_uint64),
                 ("host_ns", ctypes.c_uint64), ("gather_ns", ctypes.c_uint64),
                 ("accepted", ctypes.c_uint64), ("full_length_lanes", ctypes.c_uint64),
-                ("phase_ns", ctypes.c_uint64 * 4), ("phase_chunks", ctypes.c_uint64)]
+                ("phase_ns", ctypes.c_uint64 * 4), ("phase_chunks", ctypes.c_uint64),
+                ("auto_dedup_chunks", ctypes.c_uint64)]
 
 
 # stl_stats.phase_ns: [0] the first phase-1 kernel -- all of phase 1 when it

@@ -114,9 +114,9 @@ def test_flag_validation():
     lib = N.load()
     sig, msg, pk, bm = bytes(64), bytes(32), bytes(32), ctypes.create_string_buffer(1)
     for flags in (0, N.STL_POLICY_STELLARD_1_0_0, N.STL_FULL_LENGTH, N.STL_DEDUP_KEYS, N.STL_ONE_LANE,
-                  N.STL_DEDUP_KEYS | N.STL_ONE_LANE):
+                  N.STL_DEDUP_KEYS | N.STL_ONE_LANE, N.STL_NO_AUTO_DEDUP):
         assert lib.stl_ed25519_verify_batch(sig, msg, pk, 1, bm, flags) != N.STL_EINVAL, flags
-    assert lib.stl_ed25519_verify_batch(sig, msg, pk, 1, bm, 0x20) == N.STL_EINVAL
+    assert lib.stl_ed25519_verify_batch(sig, msg, pk, 1, bm, 0x40) == N.STL_EINVAL
     b = lib.stl_batcher_create(16, 100, N.STL_ONE_LANE)
     assert b
     lib.stl_batcher_destroy(b)

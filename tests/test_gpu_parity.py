@@ -534,6 +534,14 @@ def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
     b0, b1 = stl.words_to_bool(w0, n), stl.words_to_bool(w1, n)
     assert np.array_equal(b0, b1)
     assert np.array_equal(b1, ~bad)
+    # the host API chooses dedup by itself for these chunks (1,000 signers:
+    # the key sample repeats), and not when told not to -- same bits
+    stl.reset_stats()
+    assert np.array_equal(stl.verify_batch(s_np, m_np, p_np, policy=policy), b1)
+    assert stl.get_stats()["auto_dedup_chunks"] == -(-n // 65536)
+    stl.reset_stats()
+    assert np.array_equal(stl.verify_batch(s_np, m_np, p_np, policy=policy | stl.NO_AUTO_DEDUP), b1)
+    assert stl.get_stats()["auto_dedup_chunks"] == 0
     samp = rng.choice(n, 4000, replace=False)
     assert np.array_equal(b1[samp], oracle.verify_batch(s_np[samp], m_np[samp], p_np[samp], policy=policy & 1))
     # more distinct keys in one chunk than shared key tables (2^16): the chunk
@@ -551,3 +559,6 @@ def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
     torch.cuda.synchronize()
     assert np.array_equal(u0, u1)
     assert np.array_equal(u1, ~bad2)
+    stl.reset_stats()  # distinct keys: the host API's sample does not repeat, no dedup
+    assert np.array_equal(stl.verify_batch(s2, msgs2.cpu().numpy(), pk2.cpu().numpy(), policy=policy), u1)
+    assert stl.get_stats()["auto_dedup_chunks"] == 0
