@@ -81,8 +81,11 @@ extern "C" {
  * blob calls) choose STL_DEDUP_KEYS by themselves for every 64K-row chunk in
  * which a sample of 2,048 keys shows at least a quarter repeating (host-side,
  * about 20 us per chunk); this flag turns the automatic choice off (A/B and
- * callers that know their keys are distinct).  The device-resident calls
- * never sample (the keys are in HBM): there the caller sets STL_DEDUP_KEYS. */
+ * callers that know their keys are distinct).  stl_ed25519_verify_batch_device
+ * chooses by feedback instead (its keys are in HBM): each call ends with a
+ * one-workgroup sample of its keys on the caller's stream, and the next call
+ * on that stream follows that sample's verdict (no synchronisation; a stream's
+ * first call runs without dedup).  The bits never depend on the choice. */
 #define STL_NO_AUTO_DEDUP 0x20u
 /* Small chunks run each signature on two lanes, which ends a launch that
  * cannot fill the device sooner: the main kernel up to
@@ -345,8 +348,9 @@ typedef struct stl_stats {
    * (Straus loop), [3] fallback -- and the number of chunks timed. */
   uint64_t phase_ns[4];
   uint64_t phase_chunks;
-  /* host batch chunks that chose STL_DEDUP_KEYS by themselves (STL_NO_AUTO_DEDUP
-   * above); a struct without this field (struct_size = its offset) is accepted */
+  /* host batch chunks and device-resident calls that chose STL_DEDUP_KEYS by
+   * themselves (STL_NO_AUTO_DEDUP above); a struct without this field
+   * (struct_size = its offset) is accepted */
   uint64_t auto_dedup_chunks;
 } stl_stats;
 int stl_get_stats(stl_stats *out);

@@ -261,7 +261,15 @@ struct StreamCtx {
   // over pool streams
   hipEvent_t fork = nullptr;
   hipEvent_t join[stl::kMaxVerifyStreams] = {};
+  // device-resident automatic dedup: host-mapped word the key sample kernel
+  // writes after each call on this stream (1 = its keys repeated); the next
+  // call reads it without waiting (feedback, so a stale value only picks the
+  // other path -- the bits are the same)
+  uint32_t* auto_flag = nullptr;
+  uint32_t* auto_flag_dev = nullptr;
   void release() {
+    if (auto_flag) (void)hipHostFree(auto_flag);
+    auto_flag = auto_flag_dev = nullptr;
     ws.release();
     for (hipEvent_t& e : join) {
       if (e) (void)hipEventDestroy(e);
@@ -1270,6 +1278,40 @@ int device_for_call(Device** out) {
 }
 }  // namespace
 
+namespace {
+// The device-resident calls' automatic dedup: the keys are in
+// HBM, so instead of reading them on the host each call ends with a
+// one-workgroup sample kernel on the caller's stream whose verdict the NEXT
+// call on that stream uses -- no synchronisation, a few microseconds of GPU
+// time.  A stream's first call, or a call issued before the previous call's
+// sample has run, uses the last verdict seen (initially: no dedup).
+int auto_dedup_device(Device& d, hipStream_t s, uint32_t flags, uint32_t* mode, uint32_t** flag_dev) {
+  *flag_dev = nullptr;
+  if (!auto_dedup(flags)) return STL_OK;
+  StreamCtx& c = stream_ctx(d, s);
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (!c.auto_flag) {
+    void* p = nullptr;
+    STL_TRY(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    c.auto_flag = static_cast<uint32_t*>(p);
+    *c.auto_flag = 0;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
+      (void)hipHostFree(p);
+      c.auto_flag = nullptr;
+      return STL_EHIP;
+    }
+    c.auto_flag_dev = static_cast<uint32_t*>(dp);
+  }
+  if (__atomic_load_n(c.auto_flag, __ATOMIC_ACQUIRE) == 1u) {
+    *mode |= stl::kModeDedupKeys;
+    g_st_auto_dedup++;
+  }
+  *flag_dev = c.auto_flag_dev;
+  return STL_OK;
+}
+}  // namespace
+
 int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, const uint8_t* d_pk, size_t n,
                                     uint64_t* d_bitmap_words, uint32_t flags, void* stream) {
   if (n == 0) return STL_OK;
@@ -1279,8 +1321,12 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  return run_verify(*d, s, d_sig, d_msg, d_pk, n, d_bitmap_words, stl::kernel_mode(flags), false,
-                    g_tune_streams.load());
+  uint32_t mode = stl::kernel_mode(flags);
+  uint32_t* flag_dev = nullptr;
+  STL_RC(auto_dedup_device(*d, s, flags, &mode, &flag_dev));
+  STL_RC(run_verify(*d, s, d_sig, d_msg, d_pk, n, d_bitmap_words, mode, false, g_tune_streams.load()));
+  if (flag_dev) STL_TRY(stl::launch_key_sample(d_pk, (uint32_t)n, flag_dev, s));
+  return STL_OK;
 }
 
 int stl_debug_verify_k_device(const uint8_t* d_sig, const uint8_t* d_k, const uint8_t* d_pk, size_t n,

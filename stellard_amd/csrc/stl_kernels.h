@@ -114,6 +114,9 @@ hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint3
                           hipStream_t stream, uint32_t kind = 0u /* STL_BLOB_* */);
 // Wide base tables (stl_verify_core.h): 2 * 32769 rows of 28 words.
 constexpr size_t kWideTableBytes = 2ull * 32769 * 28 * 4;
+// Key-repeat sample of [0, n): *flag = 1 when a quarter of up to 2,048 sampled
+// keys repeat (device-resident automatic dedup; flag may be host-mapped).
+hipError_t launch_key_sample(const uint8_t* pk, uint32_t n, uint32_t* flag, hipStream_t stream);
 hipError_t launch_wide_table(uint4* out, hipStream_t stream);
 // cls / param (nullable, test data only): per-row adversarial class and its
 // parameter (stl_kernels.hip adversarial_row); msg_out receives the messages.

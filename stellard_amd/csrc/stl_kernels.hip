@@ -387,6 +387,51 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t A[8]) {
   return h * 0x7FEB352Du;
 }
 
+// Key-repeat sample of the device-resident API's automatic dedup choice
+// (stl_api.cpp, StreamCtx::auto_flag): one workgroup puts up to kSampleKeys
+// evenly spaced keys of [0, n) into an LDS table of 64-bit fingerprints and
+// writes 1 to *flag (host-mapped memory, read by the next call on the stream)
+// when at least a quarter of them repeat an earlier sampled key.  The choice
+// only selects a path: the accept bits are the same either way.
+constexpr uint32_t kSampleKeys = 2048, kSampleSlots = 4096;
+__global__ __launch_bounds__(kBlock) void key_sample_kernel(const uint8_t* __restrict__ pk, uint32_t n,
+                                                            uint32_t* __restrict__ flag) {
+  __shared__ unsigned long long tab[kSampleSlots];
+  __shared__ uint32_t dups;
+  for (uint32_t i = threadIdx.x; i < kSampleSlots; i += kBlock) tab[i] = 0;
+  if (threadIdx.x == 0) dups = 0;
+  __syncthreads();
+  const uint32_t s = n < kSampleKeys ? n : kSampleKeys;
+  for (uint32_t k = threadIdx.x; k < s; k += kBlock) {
+    uint32_t A[8];
+    ld8(A, pk + 32 * ((uint64_t)k * n / s));
+    const unsigned long long a = ((unsigned long long)A[1] << 32) | A[0];
+    const unsigned long long c = ((unsigned long long)A[7] << 32) | A[6];
+    const unsigned long long f = (a ^ (c * 0x9E3779B97F4A7C15ull)) | 1ull;  // 0 marks an empty slot
+    uint32_t h = (uint32_t)((f * 0xD6E8FEB86659FD93ull) >> 52) & (kSampleSlots - 1);
+    for (uint32_t probe = 0; probe < kSampleSlots; ++probe) {
+      const unsigned long long old = atomicCAS(&tab[h], 0ull, f);
+      if (old == 0ull) break;
+      if (old == f) {
+        atomicAdd(&dups, 1u);
+        break;
+      }
+      h = (h + 1u) & (kSampleSlots - 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // one wave writes the (uniform) verdict with a vector store
+    const uint32_t v = 4u * dups >= s ? 1u : 0u;
+    if (threadIdx.x == 0) *flag = v;
+  }
+}
+
+hipError_t launch_key_sample(const uint8_t* pk, uint32_t n, uint32_t* flag, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(key_sample_kernel, dim3(1), dim3(kBlock), 0, stream, pk, n, flag);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(kBlock) void key_insert_kernel(const uint8_t* __restrict__ pk, uint32_t base,
                                                             uint32_t cnt, uint32_t* __restrict__ slots, uint32_t mask,
                                                             uint32_t* __restrict__ rep, uint32_t* __restrict__ uid_of,

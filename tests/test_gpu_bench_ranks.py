@@ -49,4 +49,5 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert all(r["slice_bitmap_blocks_equal"] for r in c3["rank_slices"] + c4["rank_slices"])
     assert c4["rows"] == 10_000_000 and c4["digest_equal"] is True and "unequal" in c4["shards"]
     assert c5["n_ranks"] == 2 and c5["digest_equal"] is True and c5["digest_equal_dedup_keys"] is True
+    assert c5["digest_equal_no_dedup"] is True
     assert c5["byte_shards"][0][0] == 0 and c5["byte_shards"][1][1] == 1 << 20

@@ -534,6 +534,13 @@ def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
     b0, b1 = stl.words_to_bool(w0, n), stl.words_to_bool(w1, n)
     assert np.array_equal(b0, b1)
     assert np.array_equal(b1, ~bad)
+    # the device API follows the key sample of the previous call on its
+    # stream (w0's call above sampled these 1,000 signers): dedup, same bits
+    stl.reset_stats()
+    w2 = stl.verify_batch_device(*d, policy=policy)
+    torch.cuda.synchronize()
+    assert np.array_equal(stl.words_to_bool(w2, n), b1)
+    assert stl.get_stats()["auto_dedup_chunks"] == 1
     # the host API chooses dedup by itself for these chunks (1,000 signers:
     # the key sample repeats), and not when told not to -- same bits
     stl.reset_stats()
@@ -554,7 +561,12 @@ def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
     bad2 = rng.random(n2) < 0.05
     s2[bad2, 3] ^= 0x01
     d2 = [torch.from_numpy(s2).cuda(), msgs2, pk2]
+    stl.verify_batch_device(*d2, policy=policy)  # its sample: distinct keys
+    torch.cuda.synchronize()
+    stl.reset_stats()
     u0 = stl.words_to_bool(stl.verify_batch_device(*d2, policy=policy), n2)
+    torch.cuda.synchronize()
+    assert stl.get_stats()["auto_dedup_chunks"] == 0
     u1 = stl.words_to_bool(stl.verify_batch_device(*d2, policy=policy | stl.DEDUP_KEYS), n2)
     torch.cuda.synchronize()
     assert np.array_equal(u0, u1)

@@ -16,6 +16,8 @@
 #   ab:K:R:V1,V2       ABBA of libstl builds build/ab/V.so ("base" = stellard_amd/libstl.so),
 #                      tools/exec_ab.py K launches x R rotations per run, serial + 2-stream
 #   py:SCRIPT[:ARGS]   python3 tools/SCRIPT ARGS (comma-separated ARGS), stdout to OUT/SCRIPT.log
+#   exec:N:K:R:SPECS   tools/exec_ab.py on N signatures, K launches x R rotations, settings
+#                      SPECS (name=fused,queue,streams,log2 separated by +), to OUT/exec_N.json
 set -o pipefail
 OUT=$1; shift
 [ -n "$OUT" ] || { echo "usage: tools/gpujob.sh OUT STEP..."; exit 2; }
@@ -55,6 +57,10 @@ for step in "$@"; do
           >> $D/var_$v.jsonl 2>> $D/var_$v.err
         rc=$?; echo "variant $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    exec:*)
+      IFS=: read -r _ NS K R SP <<< "$step"
+      N=$NS run exec_$NS 300 python3 -u tools/exec_ab.py $K $R ${SP//+/ } || exit $?
+      cp $D/exec_$NS.log $D/exec_$NS.json ;;
     py:*)
       IFS=: read -r _ S A <<< "$step"
       run ${S%.py} 600 python3 -u tools/$S ${A//,/ } || exit $? ;;
