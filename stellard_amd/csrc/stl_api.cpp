@@ -246,8 +246,24 @@ void phase_mark(void* ctx, hipStream_t s, int i) {
 std::atomic<int> g_tune_fused{1};     // phase 1 as one kernel
 std::atomic<int> g_tune_queue{1};     // main kernel pulls units from a counter
 std::atomic<int> g_tune_streams{2};   // concurrent streams per device-resident call (A/B: DESIGN.md section 8)
-std::atomic<int> g_tune_sub_log2{18}; // signatures per stream chunk
+std::atomic<int> g_tune_sub_log2{0};  // log2 signatures per stream chunk; 0 = by batch size (chunk_for)
 std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
+
+// Chunk size of a device-resident call of n signatures over several streams
+// (DESIGN.md section 4): round(n / 2^18) chunks, at least two, of equal size
+// (a multiple of 64, above the lane-pair size), so a mid-size batch still has
+// two chunks whose phase 1 and main kernels overlap and no small remainder
+// chunk runs alone at the end; 1M signatures: four chunks of 2^18 (the
+// measured best).  STL_TUNE_CHUNK_LOG2 16..20 fixes the size instead.
+uint32_t pair_max_lanes(uint32_t grid);
+uint32_t chunk_for(uint32_t grid, size_t n) {
+  const int t = g_tune_sub_log2.load();
+  if (t) return 1u << t;
+  const size_t nc = std::max<size_t>(2, (n + ((size_t)1 << 17)) >> 18);
+  size_t sub = ((n + nc - 1) / nc + 63) / 64 * 64;
+  sub = std::max<size_t>(sub, pair_max_lanes(grid) + 64);
+  return (uint32_t)std::min<size_t>(sub, stl::kPreChunk);
+}
 
 // The verify workspace of one stream: every launch that runs kernels on a
 // stream uses that stream's workspace, in stream order -- the caller's streams
@@ -444,7 +460,8 @@ uint32_t verify_grid_for(const Device& d, size_t n) {
 
 // Largest chunk launch_verify runs on two lanes per signature: one pair wave
 // per SIMD at most (a quarter of the resident lanes).
-uint32_t pair_max(const Device& d) { return d.grid * stl::kBlock / 4; }
+uint32_t pair_max_lanes(uint32_t grid) { return grid * stl::kBlock / 4; }
+uint32_t pair_max(const Device& d) { return pair_max_lanes(d.grid); }
 
 unsigned long long* dev_counters(Device& d);
 const stl::PhaseClock* phase_clock(Device& d);
@@ -469,7 +486,7 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   x.fused_prep = g_tune_fused.load();
   x.main_queue = g_tune_queue.load() != 0;
   x.concurrent = concurrent;
-  x.sub = 1u << g_tune_sub_log2.load();
+  x.sub = chunk_for(d.grid, n);
   uint32_t S = (uint32_t)std::max(1, std::min<int>(streams, (int)stl::kMaxVerifyStreams));
   if (x.clock || n <= x.sub || x.sub <= x.pair_max) S = 1;
   S = (uint32_t)std::min<size_t>(S, (n + x.sub - 1) / x.sub);
@@ -1067,7 +1084,7 @@ int stl_debug_tuning(int key, int value) {
       if (value < 1 || value > (int)stl::kMaxVerifyStreams) return STL_EINVAL;
       return g_tune_streams.exchange(value);
     case STL_TUNE_CHUNK_LOG2:
-      if (value < 16 || value > 20) return STL_EINVAL;
+      if (value != 0 && (value < 16 || value > 20)) return STL_EINVAL;
       return g_tune_sub_log2.exchange(value);
     case STL_TUNE_BYTE_SHARDS:
       if (value != 0 && value != 1) return STL_EINVAL;

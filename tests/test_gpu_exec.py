@@ -28,7 +28,7 @@ def stl(torch_cuda):
 
 SETTINGS = [  # (fused_prep, main_queue, streams, chunk_log2)
     (0, 0, 1, 18), (1, 0, 1, 18), (0, 1, 1, 18), (1, 1, 1, 18),
-    (1, 1, 2, 18), (1, 1, 4, 18), (1, 1, 3, 17), (1, 1, 4, 16), (0, 0, 2, 19), (1, 1, 2, 20),
+    (1, 1, 2, 18), (1, 1, 4, 18), (1, 1, 3, 17), (1, 1, 4, 16), (0, 0, 2, 19), (1, 1, 2, 20), (1, 1, 2, 0),
 ]
 
 
