@@ -613,12 +613,13 @@ const uint8_t* row_key(const Batch& b, size_t i) {
 
 // Host-side estimate of key repetition over rows [lo, hi) (a
 // ledger's signers repeat -- 1,000 accounts for 100k transactions): up to
-// 2,048 evenly spaced keys, 64-bit fingerprints in an open-addressing table;
-// true when at least a quarter of the sampled keys repeat an earlier one,
-// where decoding each key once pays (key dedup).  About
-// 20 us per 64K-row chunk on the host.
+// 1,024 evenly spaced keys, 64-bit fingerprints in an open-addressing table;
+// true when at least a fifth of the sampled keys repeat an earlier one (e.g.
+// up to about 2,000 signers per 64K rows), where decoding each key once pays
+// (key dedup).  About 40 us per 64K-row chunk from cold
+// host memory, overlapped with the previous chunks' kernels.
 bool keys_repeat(const Batch& b, size_t lo, size_t hi) {
-  constexpr size_t kSample = 2048, kSlots = 4096;
+  constexpr size_t kSample = 1024, kSlots = 2048;
   const size_t n = hi - lo;
   if (n < 4 * 64) return false;
   const size_t s = std::min(n, kSample);
@@ -636,7 +637,15 @@ bool keys_repeat(const Batch& b, size_t lo, size_t hi) {
     if (table[h] == f) ++dups;
     table[h] = f;
   }
-  return 4 * dups >= s;
+  return 5 * dups >= s;
+}
+
+// The kernel mode of host rows [lo, hi): the batch's, plus key dedup when the
+// automatic choice is on and their keys repeat (counted in stl_stats).
+uint32_t chunk_policy(const Batch& b, size_t lo, size_t hi) {
+  if (!b.auto_dedup || !keys_repeat(b, lo, hi)) return b.policy;
+  g_st_auto_dedup++;
+  return b.policy | stl::kModeDedupKeys;
 }
 
 // Host-side state of one shard; lives until the batch has synchronised (the
@@ -731,25 +740,16 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
   // One stream while the phase clock is on: its per-kernel times must not
   // overlap.
   const bool two = g_tune_streams.load() > 1 && n > kPipeChunk && !phase_clock(d);
-  // automatic key dedup: chunk c's policy from a sample of its keys; the
-  // dedup-sized workspaces are taken before the first chunk, so no workspace
-  // grows while earlier chunks still run on it
-  std::vector<uint32_t> cpol((n + kPipeChunk - 1) / kPipeChunk, b.policy);
-  if (b.auto_dedup) {
-    bool any = false;
-    for (size_t c = 0; c < cpol.size(); ++c)
-      if (keys_repeat(b, lo + c * kPipeChunk, lo + std::min(n, (c + 1) * kPipeChunk))) {
-        cpol[c] |= stl::kModeDedupKeys;
-        any = true;
-        g_st_auto_dedup++;
-      }
-    if (any)
-      for (hipStream_t ks : {d.stream, d.stream2}) {
-        StreamCtx& c = stream_ctx(d, ks);
-        std::lock_guard<std::mutex> lk(c.mu);
-        STL_RC(c.ws.ensure(stl::verify_ws_bytes(d.grid, true)));
-      }
-  }
+  // automatic key dedup: each chunk's policy from a sample of its keys, taken
+  // just before the chunk is enqueued (so the sampling overlaps the earlier
+  // chunks' kernels); the dedup-sized workspaces are taken before the first
+  // chunk, so no workspace grows while earlier chunks still run on it
+  if (b.auto_dedup && n > kPipeChunk / 2)
+    for (hipStream_t ks : {d.stream, d.stream2}) {
+      StreamCtx& c = stream_ctx(d, ks);
+      std::lock_guard<std::mutex> lk(c.mu);
+      STL_RC(c.ws.ensure(stl::verify_ws_bytes(d.grid, true)));
+    }
   if (two && b.mode != Mode::kSig) STL_RC(d.ctr2.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
   for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
     const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
@@ -772,7 +772,8 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
                                   dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0, kctr,
                                   hash_grid(d), ks, b.kind));
     STL_RC(run_verify(d, ks, dsig + 64 * c0, dmsg + 32 * c0, dpk + 32 * c0, cn,
-                      static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, cpol[c0 / kPipeChunk], false, 1, two));
+                      static_cast<uint64_t*>(d.bitmap.p) + c0 / 64, chunk_policy(b, lo + c0, lo + c1), false, 1,
+                      two));
   }
   if (two) STL_RC(s.join(d.stream2, d.stream));  // results are read on d.stream
   if (dstatus && b.status) STL_TRY(hipMemcpyAsync(b.status + lo, dstatus, n, hipMemcpyDeviceToHost, d.stream));
