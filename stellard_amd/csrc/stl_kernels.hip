@@ -393,16 +393,16 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t A[8]) {
 // writes 1 to *flag (host-mapped memory, read by the next call on the stream)
 // when at least a quarter of them repeat an earlier sampled key.  The choice
 // only selects a path: the accept bits are the same either way.
-constexpr uint32_t kSampleKeys = 2048, kSampleSlots = 4096;
-__global__ __launch_bounds__(kBlock) void key_sample_kernel(const uint8_t* __restrict__ pk, uint32_t n,
-                                                            uint32_t* __restrict__ flag) {
+constexpr uint32_t kSampleKeys = 2048, kSampleSlots = 4096, kSampleBlock = 1024;
+__global__ __launch_bounds__(kSampleBlock) void key_sample_kernel(const uint8_t* __restrict__ pk, uint32_t n,
+                                                                  uint32_t* __restrict__ flag) {
   __shared__ unsigned long long tab[kSampleSlots];
   __shared__ uint32_t dups;
-  for (uint32_t i = threadIdx.x; i < kSampleSlots; i += kBlock) tab[i] = 0;
+  for (uint32_t i = threadIdx.x; i < kSampleSlots; i += kSampleBlock) tab[i] = 0;
   if (threadIdx.x == 0) dups = 0;
   __syncthreads();
   const uint32_t s = n < kSampleKeys ? n : kSampleKeys;
-  for (uint32_t k = threadIdx.x; k < s; k += kBlock) {
+  for (uint32_t k = threadIdx.x; k < s; k += kSampleBlock) {
     uint32_t A[8];
     ld8(A, pk + 32 * ((uint64_t)k * n / s));
     const unsigned long long a = ((unsigned long long)A[1] << 32) | A[0];
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(kBlock) void key_sample_kernel(const uint8_t* __res
 
 hipError_t launch_key_sample(const uint8_t* pk, uint32_t n, uint32_t* flag, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(key_sample_kernel, dim3(1), dim3(kBlock), 0, stream, pk, n, flag);
+  hipLaunchKernelGGL(key_sample_kernel, dim3(1), dim3(kSampleBlock), 0, stream, pk, n, flag);
   return hipGetLastError();
 }
 
