@@ -604,7 +604,10 @@ def gpu_run(args, world, rank, local):
                        "parallelism": f"dp{world} (index shards, RCCL bitmap gather to rank 0)"
                                       if world > 1 else "dp1",
                        "gather": gather_via, "rccl_nranks": rccl_nranks, "gather_check": gathered_check,
-                       "execution": V.execution_settings()},
+                       "execution": dict(V.execution_settings(),
+                                         stream_pool="libstl: 2 kernel + 1 copy streams per device, made in "
+                                                     "stl_init before any caller stream (DESIGN.md section 8); "
+                                                     "chunk_log2 0 = round(n / 2^18) equal chunks")},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
                          "algorithmic_bytes": BYTES_PER_VERIFY * n,

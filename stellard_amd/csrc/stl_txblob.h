@@ -41,6 +41,11 @@
 // Amounts, integers, hashes and VL payloads re-serialise byte for byte from any
 // encoding the reference constructs (STAmount.cpp:465-560), so they need no
 // check beyond their size.
+// TxnSignatures (ARRAY 3) is in no TxFormats template and not in the
+// validation template, so under kFormatTx / kFormatValidation -- every
+// product call -- a blob carrying it is DEFERRED; cutting it out of the
+// signing stream (cut_open below) only happens with kFormatNone, the bare pass
+// of the host tests (tests/test_txblob.py::test_txnsignatures_always_deferred).
 #pragma once
 #include "stl_sha512.h"
 

@@ -270,3 +270,17 @@ def test_transaction_templates(oracle, emu):
         assert constructible == (tt == 0), tt  # Payment's fields fit no other template
         decided += st != DEFERRED
     assert decided == 1
+
+
+def test_txnsignatures_always_deferred(oracle, emu):
+    """TxnSignatures (ARRAY 3, FieldNames.cpp:49-51) lies outside
+    every TxFormats template and SerializedValidation's template, so a blob
+    that carries it is always DEFERRED under the product's template checks
+    (the TxnSignatures cut of the bare pass only runs in host tests without a
+    template); the reference does not construct such a transaction either."""
+    from tests.oracle_bind import hostemu_signed_blob
+    blob = dict((n, b) for n, b, _ in T.special_cases(oracle))["with_TxnSignatures"]
+    assert not oracle.tx_blob(blob)[0]  # unconstructible in the reference
+    assert hostemu_tx_blob(emu, blob)[0] == DEFERRED
+    assert hostemu_signed_blob(emu, 0, blob)[0] == DEFERRED
+    assert hostemu_signed_blob(emu, 1, blob)[0] == DEFERRED
