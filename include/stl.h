@@ -381,7 +381,7 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
 #define STL_TUNE_STREAMS 2    /* 1..4: a device-resident verify call runs its chunks on this many
                                  concurrent streams (the caller's plus the library's own, forked
                                  and joined by events; not under stl_set_phase_timing) */
-#define STL_TUNE_CHUNK_LOG2 3 /* 16..20: log2 of the signatures per chunk when STL_TUNE_STREAMS > 1;
+#define STL_TUNE_CHUNK_LOG2 3 /* 15..20: log2 of the signatures per chunk when STL_TUNE_STREAMS > 1;
                                  0 (default): round(n / 2^18) equal chunks, at least two */
 #define STL_TUNE_BYTE_SHARDS 4 /* 1: host preimage / blob batches take the byte-balanced shard path even
                                   as one shard (test hook: runs the grouped-gather placement and

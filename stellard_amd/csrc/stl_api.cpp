@@ -254,11 +254,17 @@ std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even
 // (a multiple of 64, above the lane-pair size), so a mid-size batch still has
 // two chunks whose phase 1 and main kernels overlap and no small remainder
 // chunk runs alone at the end; 1M signatures: four chunks of 2^18 (the
-// measured best).  STL_TUNE_CHUNK_LOG2 16..20 fixes the size instead.
+// measured best).  STL_TUNE_CHUNK_LOG2 15..20 fixes the size instead.
 uint32_t pair_max_lanes(uint32_t grid);
 uint32_t chunk_for(uint32_t grid, size_t n) {
   const int t = g_tune_sub_log2.load();
   if (t) return 1u << t;
+  // up to two lane-pair chunks' worth: one chunk (its phase 1 runs as the
+  // two-role launch), measured 0.63 against 0.89 ms split at 65,536; up to
+  // three: 2 * pair_max and a lane-pair remainder (98,304: 1.01 vs 1.05 ms)
+  const size_t pm = pair_max_lanes(grid);
+  if (n <= 2 * pm) return (uint32_t)std::min<size_t>(std::max<size_t>(n, 64), stl::kPreChunk);
+  if (n <= 3 * pm) return (uint32_t)(2 * pm);
   const size_t nc = std::max<size_t>(2, (n + ((size_t)1 << 17)) >> 18);
   size_t sub = ((n + nc - 1) / nc + 63) / 64 * 64;
   sub = std::max<size_t>(sub, pair_max_lanes(grid) + 64);
@@ -949,7 +955,7 @@ int stl_init(const stl_config* cfg) {
     // profiling runs use STL_STREAMS=1 so that kernels do not overlap)
     const int s = env_int("STL_STREAMS", 0), c = env_int("STL_CHUNK_LOG2", 0);
     if (s >= 1 && s <= (int)stl::kMaxVerifyStreams) g_tune_streams.store(s);
-    if (c >= 16 && c <= 20) g_tune_sub_log2.store(c);
+    if (c >= 15 && c <= 20) g_tune_sub_log2.store(c);
   }
   int first = 0, want = -1, spd = 1;
   uint32_t cflags = 0;
@@ -1085,7 +1091,7 @@ int stl_debug_tuning(int key, int value) {
       if (value < 1 || value > (int)stl::kMaxVerifyStreams) return STL_EINVAL;
       return g_tune_streams.exchange(value);
     case STL_TUNE_CHUNK_LOG2:
-      if (value != 0 && (value < 16 || value > 20)) return STL_EINVAL;
+      if (value != 0 && (value < 15 || value > 20)) return STL_EINVAL;
       return g_tune_sub_log2.exchange(value);
     case STL_TUNE_BYTE_SHARDS:
       if (value != 0 && value != 1) return STL_EINVAL;

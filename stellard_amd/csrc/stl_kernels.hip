@@ -1312,7 +1312,7 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   // larger than the lane-pair size, and never under the phase clock
   uint32_t S = x.nstreams < kMaxVerifyStreams ? x.nstreams : kMaxVerifyStreams;
   const uint32_t sub = x.sub;
-  if (S > 1 && (x.clock != nullptr || sub > kPreChunk || (sub & 63u) != 0 || sub <= x.pair_max || n <= sub ||
+  if (S > 1 && (x.clock != nullptr || sub > kPreChunk || (sub & 63u) != 0 || n <= sub ||
                 ((uint64_t)n + sub - 1) / sub > (uint64_t)kMainQueueWords))
     S = 1;
   const uint32_t csize = S > 1 ? sub : kPreChunk;

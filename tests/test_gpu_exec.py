@@ -29,6 +29,7 @@ def stl(torch_cuda):
 SETTINGS = [  # (fused_prep, main_queue, streams, chunk_log2)
     (0, 0, 1, 18), (1, 0, 1, 18), (0, 1, 1, 18), (1, 1, 1, 18),
     (1, 1, 2, 18), (1, 1, 4, 18), (1, 1, 3, 17), (1, 1, 4, 16), (0, 0, 2, 19), (1, 1, 2, 20), (1, 1, 2, 0),
+    (1, 1, 2, 15), (1, 1, 3, 15),  # lane-pair chunks on concurrent streams
 ]
 
 
@@ -192,7 +193,7 @@ def test_tuning_rejects_bad_values(stl):
     from stellard_amd import _native as N
     lib = N.load()
     for key, bad in ((stl.TUNE_FUSED_PREP, 2), (stl.TUNE_FUSED_PREP, 3), (stl.TUNE_FUSED_PREP, -2), (stl.TUNE_MAIN_QUEUE, -2), (stl.TUNE_STREAMS, 0),
-                     (stl.TUNE_STREAMS, 5), (stl.TUNE_CHUNK_LOG2, 15), (stl.TUNE_CHUNK_LOG2, 21), (99, 1)):
+                     (stl.TUNE_STREAMS, 5), (stl.TUNE_CHUNK_LOG2, 14), (stl.TUNE_CHUNK_LOG2, 21), (99, 1)):
         assert lib.stl_debug_tuning(key, bad) == N.STL_EINVAL, (key, bad)
     assert stl.execution_settings()["streams"] in (1, 2, 3, 4)
 
