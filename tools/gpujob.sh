@@ -15,6 +15,8 @@
 #   valu               tools/valu_pmc.sh: VALUBusy / INT64 / occupancy PMC passes
 #   ab:K:R:V1,V2       ABBA of libstl builds build/ab/V.so ("base" = stellard_amd/libstl.so),
 #                      tools/exec_ab.py K launches x R rotations per run, serial + 2-stream
+#   hab:V1,V2          ABBA of the host batch API (tools/host_api_ab.py, PCIe included) over
+#                      libstl builds build/ab/V.so ("base" = stellard_amd/libstl.so)
 #   py:SCRIPT[:ARGS]   python3 tools/SCRIPT ARGS (comma-separated ARGS), stdout to OUT/SCRIPT.log
 #   exec:N:K:R:SPECS   tools/exec_ab.py on N signatures, K launches x R rotations, settings
 #                      SPECS (name=fused,queue,streams,log2 separated by +), to OUT/exec_N.json
@@ -57,6 +59,16 @@ for step in "$@"; do
           >> $D/var_$v.jsonl 2>> $D/var_$v.err
         rc=$?; echo "variant $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    hab:*)
+      IFS=, read -r -a vs <<< "${step#hab:}"
+      order=("${vs[@]}")
+      for ((i=${#vs[@]}-1; i>=0; i--)); do order+=("${vs[$i]}"); done
+      for v in "${order[@]}"; do
+        lib=""; [ "$v" != base ] && lib=build/ab/$v.so
+        STL_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/host_api_ab.py >> $D/hab.log 2>> $D/hab.err
+        rc=$?; echo "host-api variant $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done
+      tail -$(( 2 * ${#vs[@]} )) $D/hab.log ;;
     exec:*)
       IFS=: read -r _ NS K R SP <<< "$step"
       N=$NS run exec_$NS 300 python3 -u tools/exec_ab.py $K $R ${SP//+/ } || exit $?
