@@ -195,6 +195,16 @@ int stl_ed25519_verify_batch_device(const uint8_t *d_sig, const uint8_t *d_msg, 
 int stl_tx_hash_batch_device(const uint8_t *d_preimages, const uint64_t *d_offset, const uint32_t *d_len,
                              size_t n, uint8_t *d_msg, void *stream);
 
+/* Device-resident checkSign: SHA512Half(preimage_i) then verify, over rows in
+ * HBM (preimages as stl_tx_verify_batch's; d_sig n*64, d_pk n*32).  Cut into
+ * the verify's chunks and spread over the caller's stream and one of libstl's,
+ * each chunk's hashing right before its verify, so the hashing overlaps the
+ * other stream's kernels.  Bits = stl_tx_hash_batch_device followed by
+ * stl_ed25519_verify_batch_device on the same stream. */
+int stl_tx_verify_batch_device(const uint8_t *d_preimages, const uint64_t *d_offset, const uint32_t *d_len,
+                               const uint8_t *d_sig, const uint8_t *d_pk, size_t n, uint64_t *d_bitmap_words,
+                               uint32_t flags, void *stream);
+
 /* ---- serialized transactions ----
  * checkSign straight from serialized transactions -- the bytes of
  * TMTransaction.rawTransaction, or what STObject::add writes: n blobs at
@@ -250,6 +260,14 @@ int stl_tx_blob_prepare_device(const uint8_t *d_blobs, const uint64_t *d_offset,
 int stl_signed_blob_prepare_device(uint32_t kind, const uint8_t *d_blobs, const uint64_t *d_offset,
                                    const uint32_t *d_len, size_t n, uint8_t *d_msg, uint8_t *d_sig, uint8_t *d_pk,
                                    uint8_t *d_id, uint8_t *d_status, void *stream);
+/* The whole device-resident check from serialized objects in one call: the
+ * blob pass and the verify chunk by chunk over two streams (as
+ * stl_tx_verify_batch_device); d_status (n bytes) required, d_id (n*32) may be
+ * NULL.  Bits and status = stl_signed_blob_prepare_device followed by
+ * stl_ed25519_verify_batch_device. */
+int stl_signed_blob_verify_batch_device(uint32_t kind, const uint8_t *d_blobs, const uint64_t *d_offset,
+                                        const uint32_t *d_len, size_t n, uint64_t *d_bitmap_words, uint8_t *d_status,
+                                        uint8_t *d_id, uint32_t flags, void *stream);
 
 /* ---- multi-GPU: one process per GPU ----
  * Verification shards by index with no exchange; the accept bitmaps are

@@ -68,6 +68,10 @@ SYMBOLS = [
      [_U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, ctypes.c_uint32]),
     ("stl_tx_blob_prepare_device", ctypes.c_int,
      [_U8P, _P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, _U8P, _U8P, _P]),
+    ("stl_tx_verify_batch_device", ctypes.c_int,
+     [_U8P, _P, _P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
+    ("stl_signed_blob_verify_batch_device", ctypes.c_int,
+     [ctypes.c_uint32, _U8P, _P, _P, ctypes.c_size_t, _P, _U8P, _U8P, ctypes.c_uint32, _P]),
     ("stl_batcher_create", ctypes.c_void_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     ("stl_batcher_submit", ctypes.c_int, [_P, _U8P, _U8P, _U8P, _P, _P]),
     ("stl_batcher_submit_tx", ctypes.c_int, [_P, _U8P, ctypes.c_size_t, _P, _P]),

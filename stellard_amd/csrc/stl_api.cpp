@@ -289,9 +289,13 @@ struct StreamCtx {
   // other path -- the bits are the same)
   uint32_t* auto_flag = nullptr;
   uint32_t* auto_flag_dev = nullptr;
+  // the device-resident checkSign calls' verify inputs (signing hashes, and
+  // from blobs the signatures and keys), 32 or 128 B per row
+  DevBuf scratch;
   void release() {
     if (auto_flag) (void)hipHostFree(auto_flag);
     auto_flag = auto_flag_dev = nullptr;
+    scratch.release();
     ws.release();
     for (hipEvent_t& e : join) {
       if (e) (void)hipEventDestroy(e);
@@ -1335,6 +1339,139 @@ int auto_dedup_device(Device& d, hipStream_t s, uint32_t flags, uint32_t* mode, 
   return STL_OK;
 }
 }  // namespace
+
+namespace {
+// Device-resident checkSign (SURVEY 8a rows a5-a6 over rows already in HBM):
+// SHA512Half of every signing preimage -- or the serialized-object pass of
+// tx_blob_kernel -- then the verify, in the verify's chunks (chunk_for) dealt
+// to the caller's stream and pool stream 1.  The first chunk is hashed alone
+// on the caller's stream while pool stream 1 hashes all the other rows in one
+// launch (one balanced longest-first queue: per-chunk hash launches of
+// variable-length rows end in a ragged tail); chunk 0's verify then overlaps
+// that hashing, and the later chunks wait for it.  Blob rows get their
+// signature and key from the pass (deferred / malformed rows a signature that
+// always rejects); status / id as stl_tx_blob_prepare_device writes them.
+int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const uint8_t* bytes, const uint64_t* off,
+                     const uint32_t* len, const uint8_t* sig_in, const uint8_t* pk_in, size_t n, uint64_t* words,
+                     uint8_t* status, uint8_t* id, uint32_t flags) {
+  uint32_t mode = stl::kernel_mode(flags);
+  uint32_t* flag_dev = nullptr;
+  STL_RC(auto_dedup_device(d, s, flags, &mode, &flag_dev));
+  const bool dedup = (mode & stl::kModeDedupKeys) != 0;
+  const stl::PhaseClock* clock = phase_clock(d);
+  // chunks and streams as a device-resident verify call
+  size_t sub = chunk_for(d.grid, n);
+  uint32_t S = (uint32_t)std::max(1, std::min(g_tune_streams.load(), 2));
+  if (clock || n <= sub) {
+    S = 1;
+    sub = std::min<size_t>(n, stl::kPreChunk);
+  }
+  hipStream_t ks[2] = {s, s == d.stream2 ? d.stream : d.stream2};
+  StreamCtx* kc[2] = {&stream_ctx(d, ks[0]), S > 1 ? &stream_ctx(d, ks[1]) : nullptr};
+  StreamCtx& c = *kc[0];
+  uint32_t* q[2] = {nullptr, nullptr};
+  STL_RC(stream_queue(d, ks[0], S > 1 ? sub : n, &q[0]));
+  if (S > 1) STL_RC(stream_queue(d, ks[1], n - sub, &q[1]));
+  std::vector<std::unique_lock<std::mutex>> locks;
+  if (S > 1 && kc[1] < kc[0]) locks.emplace_back(kc[1]->mu);
+  locks.emplace_back(c.mu);
+  if (S > 1 && kc[1] > kc[0]) locks.emplace_back(kc[1]->mu);
+  const size_t row = blob ? 128 : 32;
+  STL_RC(c.scratch.ensure(std::max<size_t>(n, 1) * row));
+  uint8_t* msg = static_cast<uint8_t*>(c.scratch.p);
+  uint8_t* sig = blob ? msg + 32 * n : const_cast<uint8_t*>(sig_in);
+  uint8_t* pk = blob ? msg + 96 * n : const_cast<uint8_t*>(pk_in);
+  uint8_t* st = status;
+  for (uint32_t j = 0; j < S; ++j) STL_RC(kc[j]->ws.ensure(stl::verify_ws_bytes(d.grid, dedup)));
+  if (S > 1) {
+    if (!c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+    if (!c.join[1]) STL_TRY(hipEventCreateWithFlags(&c.join[1], hipEventDisableTiming));
+    if (!c.join[2]) STL_TRY(hipEventCreateWithFlags(&c.join[2], hipEventDisableTiming));
+    STL_TRY(hipEventRecord(c.fork, s));
+    STL_TRY(hipStreamWaitEvent(ks[1], c.fork, 0));
+  }
+  auto fail = [&](int rc) {
+    if (S > 1) (void)hipStreamSynchronize(ks[1]);
+    return rc;
+  };
+  // rows [b0, b0 + cnt) hashed (or passed) on stream js with queue qw
+  auto hash = [&](size_t b0, size_t cnt, hipStream_t js, uint32_t* qw) -> int {
+    if (fault_now()) return STL_EHIP;
+    hipError_t e;
+    if (blob)
+      e = stl::launch_tx_blob(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, sig + 64 * b0, pk + 32 * b0,
+                              id ? id + 32 * b0 : nullptr, st + b0, qw, hash_grid(d), js, kind);
+    else
+      e = stl::launch_tx_hash(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, qw, hash_grid(d), js);
+    return e == hipSuccess ? STL_OK : STL_EHIP;
+  };
+  if (S == 1) {
+    STL_RC(hash(0, n, s, q[0]));
+  } else {
+    int rc = hash(0, sub, ks[0], q[0]);
+    if (!rc) rc = hash(sub, n - sub, ks[1], q[1]);
+    if (!rc && hipEventRecord(c.join[2], ks[1]) != hipSuccess) rc = STL_EHIP;
+    if (rc) return fail(rc);
+  }
+  size_t k = 0;
+  for (size_t b0 = 0; b0 < n; b0 += sub, ++k) {
+    const uint32_t j = (uint32_t)(k % S);
+    const uint32_t cnt = (uint32_t)std::min(sub, n - b0);
+    hipStream_t js = ks[j];
+    // the caller's stream verifies chunk 0 during the other rows' hashing,
+    // then waits for it
+    if (S > 1 && k == 2 && hipStreamWaitEvent(ks[0], c.join[2], 0) != hipSuccess) return fail(STL_EHIP);
+    stl::VerifyExec x;
+    x.grid = verify_grid_for(d, cnt);
+    x.pair_max = pair_max(d);
+    x.wide = static_cast<const uint4*>(d.wide.p);
+    x.counters = dev_counters(d);
+    x.clock = S > 1 ? nullptr : clock;
+    x.fused_prep = g_tune_fused.load();
+    x.main_queue = g_tune_queue.load() != 0;
+    x.concurrent = S > 1;
+    x.nstreams = 1;
+    x.streams[0] = js;
+    x.ws[0] = static_cast<uint4*>(kc[j]->ws.p);
+    if (fault_now() || stl::launch_verify(sig + 64 * b0, msg + 32 * b0, pk + 32 * b0, cnt, words + b0 / 64, mode,
+                                          false, x) != hipSuccess)
+      return fail(STL_EHIP);
+  }
+  if (S > 1) {
+    if (hipEventRecord(c.join[1], ks[1]) != hipSuccess || hipStreamWaitEvent(s, c.join[1], 0) != hipSuccess)
+      return fail(STL_EHIP);
+  }
+  if (flag_dev) STL_TRY(stl::launch_key_sample(pk, (uint32_t)n, flag_dev, s));
+  return STL_OK;
+}
+}  // namespace
+
+int stl_tx_verify_batch_device(const uint8_t* d_preimages, const uint64_t* d_offset, const uint32_t* d_len,
+                               const uint8_t* d_sig, const uint8_t* d_pk, size_t n, uint64_t* d_bitmap_words,
+                               uint32_t flags, void* stream) {
+  if (n == 0) return STL_OK;
+  if (!d_preimages || !d_offset || !d_len || !d_sig || !d_pk || !d_bitmap_words) return STL_EINVAL;
+  STL_RC(check_flags(flags));
+  if (n > 0xffffffc0ull) return STL_EINVAL;
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
+  return checksign_device(*d, static_cast<hipStream_t>(stream), false, 0u, d_preimages, d_offset, d_len, d_sig, d_pk,
+                          n, d_bitmap_words, nullptr, nullptr, flags);
+}
+
+int stl_signed_blob_verify_batch_device(uint32_t kind, const uint8_t* d_blobs, const uint64_t* d_offset,
+                                        const uint32_t* d_len, size_t n, uint64_t* d_bitmap_words, uint8_t* d_status,
+                                        uint8_t* d_id, uint32_t flags, void* stream) {
+  if (kind != STL_BLOB_TRANSACTION && kind != STL_BLOB_VALIDATION) return STL_EINVAL;
+  if (n == 0) return STL_OK;
+  if (!d_blobs || !d_offset || !d_len || !d_bitmap_words || !d_status) return STL_EINVAL;
+  STL_RC(check_flags(flags));
+  if (n > 0xffffffc0ull) return STL_EINVAL;
+  Device* d = nullptr;
+  STL_RC(device_for_call(&d));
+  return checksign_device(*d, static_cast<hipStream_t>(stream), true, kind, d_blobs, d_offset, d_len, nullptr,
+                          nullptr, n, d_bitmap_words, d_status, d_id, flags);
+}
 
 int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, const uint8_t* d_pk, size_t n,
                                     uint64_t* d_bitmap_words, uint32_t flags, void* stream) {

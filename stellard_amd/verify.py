@@ -316,6 +316,51 @@ def tx_hash_batch_device(preimages, offsets, lengths, out_msg=None, stream=None)
     return out_msg
 
 
+def _check_rows(*ts):
+    import torch
+    for t in ts:
+        if t is not None and (not t.is_cuda or not t.is_contiguous()):
+            raise ValueError("device entry point needs contiguous CUDA tensors")
+    if ts[1].dtype != torch.int64 or ts[2].dtype != torch.int32:
+        raise ValueError("offsets must be int64 and lengths int32")
+
+
+def tx_verify_batch_device(preimages, offsets, lengths, sig, pk, out_words=None, policy=POLICY_SODIUM_1_0_18,
+                           stream=None):
+    """stl_tx_verify_batch_device: the device-resident checkSign in one call --
+    SHA512Half of each preimage and the verify, chunk by chunk over two
+    streams -> int64 bitmap words (same bits as tx_hash_batch_device +
+    verify_batch_device)."""
+    import torch
+    n = offsets.shape[0]
+    if out_words is None:
+        out_words = torch.empty(((n + 63) // 64,), dtype=torch.int64, device=preimages.device)
+    _check_rows(preimages, offsets, lengths, sig, pk, out_words)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    N.check(N.load().stl_tx_verify_batch_device(p(preimages), p(offsets), p(lengths), p(sig), p(pk), n, p(out_words),
+                                                policy, _stream_ptr(stream)), "stl_tx_verify_batch_device")
+    return out_words
+
+
+def signed_blob_verify_batch_device(blobs, offsets, lengths, out_words=None, tx_ids=False,
+                                    policy=POLICY_SODIUM_1_0_18, stream=None, kind=None):
+    """stl_signed_blob_verify_batch_device: checkSign from serialized objects
+    in HBM in one call -> dict of words (bitmap), status and (tx_ids) tx_id."""
+    import torch
+    n = offsets.shape[0]
+    dev = blobs.device
+    if out_words is None:
+        out_words = torch.empty(((n + 63) // 64,), dtype=torch.int64, device=dev)
+    status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    tx_id = torch.empty((n, 32), dtype=torch.uint8, device=dev) if tx_ids else None
+    _check_rows(blobs, offsets, lengths, out_words)
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    N.check(N.load().stl_signed_blob_verify_batch_device(
+        N.STL_BLOB_TRANSACTION if kind is None else kind, p(blobs), p(offsets), p(lengths), n, p(out_words),
+        p(status), p(tx_id), policy, _stream_ptr(stream)), "stl_signed_blob_verify_batch_device")
+    return {"words": out_words, "status": status, "tx_id": tx_id}
+
+
 def tx_blob_prepare_device(blobs, offsets, lengths, tx_ids=True, stream=None, kind=None):
     """Serialized transactions already in HBM (uint8 / int64 / int32 CUDA
     tensors) -> dict of msg (n,32), sig (n,64), pk (n,32), status (n,) and

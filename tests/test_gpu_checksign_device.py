@@ -1,0 +1,167 @@
+"""Device-resident checkSign in one call (stl_tx_verify_batch_device,
+stl_signed_blob_verify_batch_device; SerializedTransaction::checkSign,
+SerializedTransaction.cpp:220-230, over rows already in HBM): the hashing and
+the verify chunk by chunk over two streams must give exactly the bits of the
+two-step path (tx_hash_batch_device / tx_blob_prepare_device, then
+verify_batch_device), which the other GPU tests pin to the oracle -- and, on
+the full config-5 ledger, libsodium's committed bitmap digest.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120
+"""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from tests import datasets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def stl(torch_cuda):
+    from stellard_amd import verify
+    verify.init()
+    return verify
+
+
+@pytest.fixture(scope="module")
+def ledger(stl, torch_cuda):
+    """The config-5 ledger of tests/datasets.py on the device, invalid rows
+    flipped after signing (the construction of the committed digest)."""
+    torch = torch_cuda
+    lp = datasets.ledger_plan()
+    d_pre = torch.from_numpy(lp["pre"]).cuda()
+    d_off = torch.from_numpy(lp["offs"]).cuda()
+    d_len = torch.from_numpy(lp["lens"]).cuda()
+    seeds = torch.from_numpy(np.ascontiguousarray(lp["signers"][lp["who"]])).cuda()
+    msgs = stl.tx_hash_batch_device(d_pre, d_off, d_len)
+    pk, sig = stl.sign_batch_device(seeds, msgs)
+    (pos, pbit), (srow, scol, sbit) = datasets.ledger_mutations(lp)
+    d_pre[torch.from_numpy(pos).cuda()] ^= torch.from_numpy(pbit).cuda()
+    sig[torch.from_numpy(srow).cuda(), torch.from_numpy(scol).cuda()] ^= torch.from_numpy(sbit).cuda()
+    torch.cuda.synchronize()
+    return lp, d_pre, d_off, d_len, sig, pk
+
+
+def _digest(stl, words, n):
+    b = np.packbits(stl.words_to_bool(words, n), bitorder="little")
+    return hashlib.sha256(b.tobytes()).hexdigest()
+
+
+@pytest.mark.timeout(300)
+def test_tx_verify_device_ledger_digest(stl, torch_cuda, ledger):
+    """The whole 2^20-transaction ledger: one call equals libsodium's digest,
+    under every dedup choice and execution setting, and equals the two-step
+    path on sub-ranges (ragged sizes, both sides of the chunking rules)."""
+    torch = torch_cuda
+    lp, d_pre, d_off, d_len, sig, pk = ledger
+    n = lp["n"]
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)["config5"]["bitmap_sha256"]
+    for flags in (0, stl.DEDUP_KEYS, stl.NO_AUTO_DEDUP, 0):
+        w = stl.tx_verify_batch_device(d_pre, d_off, d_len, sig, pk, policy=flags)
+        torch.cuda.synchronize()
+        assert _digest(stl, w, n) == want, flags
+    old = stl.debug_tuning(stl.TUNE_STREAMS, 1)
+    try:
+        w = stl.tx_verify_batch_device(d_pre, d_off, d_len, sig, pk)
+        torch.cuda.synchronize()
+        assert _digest(stl, w, n) == want
+    finally:
+        stl.debug_tuning(stl.TUNE_STREAMS, old)
+    stl.set_phase_timing(True)
+    try:
+        w = stl.tx_verify_batch_device(d_pre, d_off, d_len, sig, pk)
+        torch.cuda.synchronize()
+        assert _digest(stl, w, n) == want
+    finally:
+        stl.set_phase_timing(False)
+    for lo, m in ((0, 1), (64, 1000), (4096, 65536), (128, 70001), (640, 98304), (1 << 19, 300_001)):
+        sl = slice(lo, lo + m)
+        two = stl.verify_batch_device(sig[sl], stl.tx_hash_batch_device(d_pre, d_off[sl], d_len[sl]), pk[sl])
+        one = stl.tx_verify_batch_device(d_pre, d_off[sl], d_len[sl], sig[sl], pk[sl])
+        torch.cuda.synchronize()
+        assert np.array_equal(stl.words_to_bool(one, m), stl.words_to_bool(two, m)), (lo, m)
+
+
+@pytest.mark.timeout(300)
+def test_signed_blob_verify_device_equals_two_step(stl, torch_cuda):
+    """Serialized Payment transactions (1,000 signers; 3 % with a flipped
+    byte anywhere in the blob, so some become deferred or malformed): bits,
+    status and transaction ids of the one-call path equal the prepare + verify
+    path, for transaction and validation kinds and several batch sizes."""
+    torch = torch_cuda
+    from tools.payments import blobs_from_preimages, pack, payment_preimages
+    rng = np.random.default_rng(0xB10B)
+    nacc, n = 1000, 150_000
+    acc_seeds = rng.integers(0, 256, (nacc, 32), dtype=np.uint8)
+    apk, _ = stl.sign_batch_device(torch.from_numpy(acc_seeds).cuda(), torch.zeros((nacc, 32), dtype=torch.uint8,
+                                                                                       device="cuda"))
+    pre = payment_preimages(apk.cpu().numpy(), n, rng)
+    pbuf, poff, plen = pack(pre)
+    msgs = stl.tx_hash_batch_device(torch.from_numpy(pbuf).cuda(), torch.from_numpy(poff.view(np.int64)).cuda(),
+                                    torch.from_numpy(plen.view(np.int32)).cuda())
+    tpk, tsig = stl.sign_batch_device(torch.from_numpy(acc_seeds[np.arange(n) % nacc]).cuda(), msgs)
+    torch.cuda.synchronize()
+    blobs = blobs_from_preimages(pre, tsig.cpu().numpy(), tpk.cpu().numpy())
+    buf, offs, lens = pack(blobs)
+    buf = np.concatenate([buf, np.zeros(4, np.uint8)])
+    bad = rng.choice(n, n * 3 // 100, replace=False)
+    for i in bad:
+        buf[int(offs[i]) + int(rng.integers(0, int(lens[i])))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    d_buf = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+    for kind in (0, 1):  # STL_BLOB_TRANSACTION, STL_BLOB_VALIDATION
+        for m in (n, 65_536, 1_000, 100_001):
+            sl = slice(0, m)
+            o = stl.tx_blob_prepare_device(d_buf, d_off[sl], d_len[sl], tx_ids=True, kind=kind)
+            two = stl.verify_batch_device(o["sig"], o["msg"], o["pk"])
+            one = stl.signed_blob_verify_batch_device(d_buf, d_off[sl], d_len[sl], tx_ids=True, kind=kind)
+            torch.cuda.synchronize()
+            b1, b2 = stl.words_to_bool(one["words"], m), stl.words_to_bool(two, m)
+            assert np.array_equal(b1, b2), (kind, m)
+            assert torch.equal(one["status"], o["status"]), (kind, m)
+            assert torch.equal(one["tx_id"], o["tx_id"]), (kind, m)
+            if kind == 0 and m == n:
+                st = o["status"].cpu().numpy()
+                assert b1.sum() > 0.9 * n and (st != 0).sum() > 0  # mostly valid; some deferred / malformed
+
+
+def test_checksign_device_faults_are_errors(stl, torch_cuda, ledger):
+    """A failure injected at any HIP call of the one-call path returns a
+    negative code, never a reject bitmap, and the next clean call is exact."""
+    from stellard_amd import _native as N
+    torch = torch_cuda
+    lp, d_pre, d_off, d_len, sig, pk = ledger
+    m = 200_000
+    sl = slice(0, m)
+    ref = stl.words_to_bool(stl.tx_verify_batch_device(d_pre, d_off[sl], d_len[sl], sig[sl], pk[sl]), m)
+    torch.cuda.synchronize()
+    for k in range(0, 12):
+        stl.debug_fault_after(k)
+        try:
+            w = stl.tx_verify_batch_device(d_pre, d_off[sl], d_len[sl], sig[sl], pk[sl])
+            torch.cuda.synchronize()
+            ok = True
+        except N.StlError as e:
+            ok = False
+            assert e.rc < -1
+        finally:
+            stl.debug_fault_after(-1)
+        torch.cuda.synchronize()
+        if ok:
+            assert np.array_equal(stl.words_to_bool(w, m), ref), k
+        w = stl.tx_verify_batch_device(d_pre, d_off[sl], d_len[sl], sig[sl], pk[sl])
+        torch.cuda.synchronize()
+        assert np.array_equal(stl.words_to_bool(w, m), ref), k

@@ -280,8 +280,11 @@ def ledger_leg(ctx, reps=5):
     if not all(o for _, o in st):
         return {"error": f"ledger input digest differs on ranks {[r for r, (_, o) in enumerate(st) if not o]}"}
 
-    def step(flags):
-        if m:
+    def step(flags, fused=True):
+        if m and fused:  # one call: hashing and verify chunk by chunk over two streams
+            V.tx_verify_batch_device(d_pre, d_off[lo:hi], d_len[lo:hi], sig[lo:hi], pk[lo:hi], out_words=words,
+                                     policy=flags, stream=stream)
+        elif m:
             V.tx_hash_batch_device(d_pre, d_off[lo:hi], d_len[lo:hi], out_msg=m5[lo:hi], stream=stream)
             V.verify_batch_device(sig[lo:hi], m5[lo:hi], pk[lo:hi], out_words=words, policy=flags, stream=stream)
         ctx["gather"](words, offs, full)
@@ -299,6 +302,11 @@ def ledger_leg(ctx, reps=5):
         res["ms" + label] = dt * 1e3
         if rank == 0:
             res["digest_equal" + label] = bitmap_sha256(full, n) == want["bitmap_sha256"]
+    # the two-step path (tx_hash_batch_device, then verify_batch_device) for comparison
+    dt = timed(ctx, lambda: step(0, fused=False), reps)
+    res["tx_per_s_two_step"] = n / dt
+    if rank == 0:
+        res["digest_equal_two_step"] = bitmap_sha256(full, n) == want["bitmap_sha256"]
     pre_bytes = [int(lp["offs"][b[1] - 1] + lp["lens"][b[1] - 1] - lp["offs"][b[0]]) if b[1] > b[0] else 0
                  for b in bounds]
     out = {"transactions": n, "n_ranks": world, "scaling": "strong (one ledger split across the ranks)",
@@ -308,7 +316,8 @@ def ledger_leg(ctx, reps=5):
            "data": "tests/datasets.py ledger_plan: 'STX\\0' + random bytes, lengths log-uniform in [113, 4096], "
                    "1,000 signers, GPU-signed over SHA512Half, 2 % of the rows with a preimage / R / S bit "
                    "flipped after signing; every rank builds the whole ledger and checks its input digest",
-           "timing": "barrier, SHA512Half + verify of the rank's byte shard + gather to rank 0 "
+           "timing": "barrier, SHA512Half + verify of the rank's byte shard (stl_tx_verify_batch_device; "
+                     "tx_per_s_two_step: tx_hash_batch_device then verify_batch_device) + gather to rank 0 "
                      "(stl_bitmap_gatherv_device), sync, barrier; median, max over ranks"}
     if rank == 0:
         out.update({"accepted_expected": want["accepted"], "bitmap_sha256_expected": want["bitmap_sha256"]})
