@@ -619,7 +619,13 @@ def gpu_run(args, world, rank, local):
                        "execution": dict(V.execution_settings(),
                                          stream_pool="libstl: 2 kernel + 1 copy streams per device, made in "
                                                      "stl_init before any caller stream (DESIGN.md section 8); "
-                                                     "chunk_log2 0 = round(n / 2^18) equal chunks")},
+                                                     "chunk_log2 0 = round(n / 2^18) equal chunks",
+                                         overlap={"serial_kernel_sum_ms": sum(phase_ms.values()),
+                                                  "launch_ms": kern_ms,
+                                                  "ratio": kern_ms / max(1e-9, sum(phase_ms.values())),
+                                                  "reading": "ratio < 1: the chunks on the pool's two kernel "
+                                                             "streams overlapped; >= 1: they ran one after "
+                                                             "another (e.g. streams sharing a hardware queue)"})},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
                          "algorithmic_bytes": BYTES_PER_VERIFY * n,

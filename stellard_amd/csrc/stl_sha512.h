@@ -8,7 +8,8 @@
 //     (Serializer.cpp:354-360 via STObject::getSigningHash,
 //     SerializedObject.cpp:444-450): 1..33 blocks for 100 B .. 4 KB preimages.
 // 64-bit words on 32-bit ALUs: the compiler lowers rotates to v_alignbit_b32
-// pairs and adds to v_add_co/v_addc pairs.
+// pairs and adds to v_add_co/v_addc pairs; xor3 / ch / maj are one
+// v_bitop3_b32 per half.
 #pragma once
 #include "stl_fe25519.h"
 
@@ -81,7 +82,25 @@ STL_HD W64 shr(W64 x) {
   return W64{abit(x.hi, x.lo, N), x.hi >> N};
 }
 
-STL_HD W64 xor3(W64 a, W64 b, W64 c) { return W64{a.lo ^ b.lo ^ c.lo, a.hi ^ b.hi ^ c.hi}; }
+// Any three-input bitwise function as one v_bitop3_b32 (gfx950): IMM is its
+// truth table, bit (a << 2 | b << 1 | c) = f(a, b, c).  The compiler does not
+// fuse a three-way xor by itself here (two v_xor_b32 per half), which made
+// the xors the largest instruction group of a compression.
+template <uint32_t IMM>
+STL_HD uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+#else
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < 8; ++i)
+    if ((IMM >> i) & 1u) r |= ((i & 4u) ? a : ~a) & ((i & 2u) ? b : ~b) & ((i & 1u) ? c : ~c);
+  return r;
+#endif
+}
+
+STL_HD W64 xor3(W64 a, W64 b, W64 c) {
+  return W64{bitop3<0x96u>(a.lo, b.lo, c.lo), bitop3<0x96u>(a.hi, b.hi, c.hi)};
+}
 
 STL_HD W64 add(W64 a, W64 b) {
   unsigned c;
@@ -90,13 +109,10 @@ STL_HD W64 add(W64 a, W64 b) {
   return W64{lo, hi};
 }
 
-// (e & f) ^ (~e & g): v_bfi_b32 per half
-STL_HD W64 ch(W64 e, W64 f, W64 g) { return W64{(e.lo & f.lo) | (~e.lo & g.lo), (e.hi & f.hi) | (~e.hi & g.hi)}; }
-// majority = bfi(a ^ b, c, b)
-STL_HD W64 maj(W64 a, W64 b, W64 c) {
-  const uint32_t xl = a.lo ^ b.lo, xh = a.hi ^ b.hi;
-  return W64{(xl & c.lo) | (~xl & b.lo), (xh & c.hi) | (~xh & b.hi)};
-}
+// (e & f) ^ (~e & g) = e ? f : g, one bitop3 per half
+STL_HD W64 ch(W64 e, W64 f, W64 g) { return W64{bitop3<0xCAu>(e.lo, f.lo, g.lo), bitop3<0xCAu>(e.hi, f.hi, g.hi)}; }
+// majority, one bitop3 per half
+STL_HD W64 maj(W64 a, W64 b, W64 c) { return W64{bitop3<0xE8u>(a.lo, b.lo, c.lo), bitop3<0xE8u>(a.hi, b.hi, c.hi)}; }
 
 // Round constant, pinned per round as a scalar pair (see the loop below).
 STL_HD W64 sha_kw(int i) {

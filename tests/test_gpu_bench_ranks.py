@@ -51,3 +51,6 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert c5["n_ranks"] == 2 and c5["digest_equal"] is True and c5["digest_equal_dedup_keys"] is True
     assert c5["digest_equal_no_dedup"] is True
     assert c5["byte_shards"][0][0] == 0 and c5["byte_shards"][1][1] == 1 << 20
+    sl = c5["small_ledgers"]
+    assert sl["bits_equal_expected"] is True and sl["transactions"] == 1 << 20
+    assert 1000 <= sl["ledger_size"]["median"] <= 20000 and sl["latency_ms"]["p50"] > 0
