@@ -1369,6 +1369,27 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   hipStream_t ks[2] = {s, s == d.stream2 ? d.stream : d.stream2};
   StreamCtx* kc[2] = {&stream_ctx(d, ks[0]), S > 1 ? &stream_ctx(d, ks[1]) : nullptr};
   StreamCtx& c = *kc[0];
+  // One chunk whose phase 1 runs as the two-role lane-pair kernel (small
+  // batches; not blobs, whose signatures and keys come out of the pass): its
+  // point role -- the two square-root chains, which need no message -- and
+  // the key sample run on the other pool stream while the preimages hash.
+  auto exec_for = [&](uint32_t cnt, uint32_t j) {
+    stl::VerifyExec x;
+    x.grid = verify_grid_for(d, cnt);
+    x.pair_max = pair_max(d);
+    x.wide = static_cast<const uint4*>(d.wide.p);
+    x.counters = dev_counters(d);
+    x.clock = S > 1 ? nullptr : clock;
+    x.fused_prep = g_tune_fused.load();
+    x.main_queue = g_tune_queue.load() != 0;
+    x.concurrent = S > 1;
+    x.nstreams = 1;
+    x.streams[0] = ks[j];
+    x.ws[0] = static_cast<uint4*>(kc[j]->ws.p);
+    return x;
+  };
+  const bool ahead = S == 1 && !blob && !clock && n <= stl::kPreChunk &&
+                     stl::verify_pair_points((uint32_t)n, mode, exec_for((uint32_t)n, 0));
   uint32_t* q[2] = {nullptr, nullptr};
   STL_RC(stream_queue(d, ks[0], S > 1 ? sub : n, &q[0]));
   if (S > 1) STL_RC(stream_queue(d, ks[1], n - sub, &q[1]));
@@ -1383,7 +1404,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   uint8_t* pk = blob ? msg + 96 * n : const_cast<uint8_t*>(pk_in);
   uint8_t* st = status;
   for (uint32_t j = 0; j < S; ++j) STL_RC(kc[j]->ws.ensure(stl::verify_ws_bytes(d.grid, dedup)));
-  if (S > 1) {
+  if (S > 1 || ahead) {
     if (!c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
     if (!c.join[1]) STL_TRY(hipEventCreateWithFlags(&c.join[1], hipEventDisableTiming));
     if (!c.join[2]) STL_TRY(hipEventCreateWithFlags(&c.join[2], hipEventDisableTiming));
@@ -1391,9 +1412,18 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     STL_TRY(hipStreamWaitEvent(ks[1], c.fork, 0));
   }
   auto fail = [&](int rc) {
-    if (S > 1) (void)hipStreamSynchronize(ks[1]);
+    if (S > 1 || ahead) (void)hipStreamSynchronize(ks[1]);
     return rc;
   };
+  if (ahead) {
+    int rc = STL_OK;
+    if (fault_now() || stl::launch_verify_points(sig, pk, (uint32_t)n, mode, exec_for((uint32_t)n, 0), ks[1]) !=
+                           hipSuccess)
+      rc = STL_EHIP;
+    if (!rc && flag_dev && stl::launch_key_sample(pk, (uint32_t)n, flag_dev, ks[1]) != hipSuccess) rc = STL_EHIP;
+    if (!rc && hipEventRecord(c.join[2], ks[1]) != hipSuccess) rc = STL_EHIP;
+    if (rc) return fail(rc);
+  }
   // rows [b0, b0 + cnt) hashed (or passed) on stream js with queue qw
   auto hash = [&](size_t b0, size_t cnt, hipStream_t js, uint32_t* qw) -> int {
     if (fault_now()) return STL_EHIP;
@@ -1406,7 +1436,9 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     return e == hipSuccess ? STL_OK : STL_EHIP;
   };
   if (S == 1) {
-    STL_RC(hash(0, n, s, q[0]));
+    int rc = hash(0, n, s, q[0]);
+    if (!rc && ahead && hipStreamWaitEvent(s, c.join[2], 0) != hipSuccess) rc = STL_EHIP;
+    if (rc) return fail(rc);
   } else {
     int rc = hash(0, sub, ks[0], q[0]);
     if (!rc) rc = hash(sub, n - sub, ks[1], q[1]);
@@ -1421,18 +1453,8 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     // the caller's stream verifies chunk 0 during the other rows' hashing,
     // then waits for it
     if (S > 1 && k == 2 && hipStreamWaitEvent(ks[0], c.join[2], 0) != hipSuccess) return fail(STL_EHIP);
-    stl::VerifyExec x;
-    x.grid = verify_grid_for(d, cnt);
-    x.pair_max = pair_max(d);
-    x.wide = static_cast<const uint4*>(d.wide.p);
-    x.counters = dev_counters(d);
-    x.clock = S > 1 ? nullptr : clock;
-    x.fused_prep = g_tune_fused.load();
-    x.main_queue = g_tune_queue.load() != 0;
-    x.concurrent = S > 1;
-    x.nstreams = 1;
-    x.streams[0] = js;
-    x.ws[0] = static_cast<uint4*>(kc[j]->ws.p);
+    stl::VerifyExec x = exec_for(cnt, j);
+    x.points_done = ahead;
     if (fault_now() || stl::launch_verify(sig + 64 * b0, msg + 32 * b0, pk + 32 * b0, cnt, words + b0 / 64, mode,
                                           false, x) != hipSuccess)
       return fail(STL_EHIP);
@@ -1441,7 +1463,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     if (hipEventRecord(c.join[1], ks[1]) != hipSuccess || hipStreamWaitEvent(s, c.join[1], 0) != hipSuccess)
       return fail(STL_EHIP);
   }
-  if (flag_dev) STL_TRY(stl::launch_key_sample(pk, (uint32_t)n, flag_dev, s));
+  if (flag_dev && !ahead) STL_TRY(stl::launch_key_sample(pk, (uint32_t)n, flag_dev, s));
   return STL_OK;
 }
 }  // namespace

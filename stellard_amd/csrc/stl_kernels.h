@@ -96,7 +96,17 @@ struct VerifyExec {
   uint4* ws[kMaxVerifyStreams] = {};    // verify_ws_bytes(grid, dedup) each
   hipEvent_t fork = nullptr;
   hipEvent_t join[kMaxVerifyStreams] = {};
+  bool points_done = false;             // one lane-pair chunk whose point role already ran
+                                        // (launch_verify_points, ordered before this launch)
 };
+// Whether launch_verify of n <= kPreChunk signatures (one chunk) runs its
+// phase 1 as the two-role lane-pair kernel -- then its point role (the two
+// square-root chains; needs only the signatures and keys) may be launched
+// ahead by launch_verify_points, e.g. while the messages are still being
+// hashed, and launch_verify with points_done runs only the scalar role.
+bool verify_pair_points(uint32_t n, uint32_t policy, const VerifyExec& x);
+hipError_t launch_verify_points(const uint8_t* sig, const uint8_t* pk, uint32_t n, uint32_t policy,
+                                const VerifyExec& x, hipStream_t stream);
 hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint8_t* pk, uint32_t n,
                          uint64_t* bitmap, uint32_t policy, bool pre_k, const VerifyExec& x);
 hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t* m, const uint64_t* moff,

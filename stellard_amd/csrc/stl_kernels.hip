@@ -1183,6 +1183,42 @@ hipError_t launch_wide_table(uint4* out, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Small chunks: two lanes per signature in the point decodings and the main
+// kernel (verify_prep_pair_kernel, verify_main_pair_kernel); the bits are the
+// same.  It also takes precedence over key dedup: a chunk this small is
+// latency-bound, and measured 0.46-0.52 ms on pairs against 0.68-0.75 ms
+// deduplicated (1,000 signers).
+static bool pair_chunk(uint32_t cnt, uint32_t policy, const VerifyExec& x) {
+  return (policy & kModeOneLane) == 0 && cnt <= x.pair_max && 2ull * cnt <= (uint64_t)x.grid * kBlock;
+}
+
+// The point decodings' pairs split the two square roots without duplicating
+// work, so they pay up to twice that size (two pair waves per SIMD; no
+// workspace), ahead of the one-lane main kernel (verify_finish_pair_kernel in
+// between).
+static bool pair_point_chunk(uint32_t cnt, uint32_t policy, const VerifyExec& x) {
+  const bool dedup = (policy & kModeDedupKeys) != 0;
+  return pair_chunk(cnt, policy, x) ||
+         (!x.concurrent && (policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * x.pair_max);
+}
+
+bool verify_pair_points(uint32_t n, uint32_t policy, const VerifyExec& x) {
+  return n > 0 && n <= kPreChunk && pair_point_chunk(n, policy, x);
+}
+
+// The point role of verify_prep_pair_kernel alone (nbs = 0: every block is a
+// point block) for rows [0, n), into the phase-1 state of x.ws[0] -- where
+// launch_verify's single chunk reads it.
+hipError_t launch_verify_points(const uint8_t* sig, const uint8_t* pk, uint32_t n, uint32_t policy,
+                                const VerifyExec& x, hipStream_t stream) {
+  if (!verify_pair_points(n, policy, x)) return hipErrorInvalidValue;
+  uint4* pre = x.ws[0] + (size_t)x.grid * (kWsBytesPerBlock / 16);
+  const dim3 gp((2 * n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(verify_prep_pair_kernel<false>, gp, dim3(kBlock), 0, stream, sig, nullptr, pk, 0u, n, policy,
+                     pre, 0u);
+  return hipGetLastError();
+}
+
 // One chunk (<= kPreChunk signatures at [base, base+cnt)) on one stream and
 // workspace: phase 1, main, fallback.  `qctr` is the chunk's zeroed counter
 // of the main kernel's unit queue.
@@ -1215,17 +1251,8 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     const uint32_t units = (cnt + 63) / 64;
     const uint32_t wgs = (units + kBlock / 64 - 1) / (kBlock / 64);
     const dim3 g2(wgs < grid ? wgs : grid);
-    // Small chunks: two lanes per signature in the point decodings and the main
-    // kernel (verify_prep_pair_kernel, verify_main_pair_kernel); the bits are the
-    // same.  It also takes precedence over key dedup: a chunk this small is
-    // latency-bound, and measured 0.46-0.52 ms on pairs against 0.68-0.75 ms
-    // deduplicated (1,000 signers).
-    const bool pair = (policy & kModeOneLane) == 0 && cnt <= pair_max && 2ull * cnt <= (uint64_t)grid * kBlock;
-    // The point decodings' pairs split the two square roots without
-    // duplicating work, so they pay up to twice that size (two pair waves per
-    // SIMD; no workspace), ahead of the one-lane main kernel
-    // (verify_finish_pair_kernel in between).
-    const bool pair_point = pair || (!x.concurrent && (policy & kModeOneLane) == 0 && !dedup && cnt <= 2ull * pair_max);
+    const bool pair = pair_chunk(cnt, policy, x);
+    const bool pair_point = pair_point_chunk(cnt, policy, x);
     const dim3 gp((2 * cnt + kBlock - 1) / kBlock);
     const bool fused = x.fused_prep != 0 && !pair_point && !dedup;
     mark(0);
@@ -1233,13 +1260,15 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     if (pair_point) {
       // both halves of phase 1 in one launch, side by side (verify_prep_pair_kernel);
       // the main pair kernel finishes the state itself, the one-lane main
-      // kernel gets it from verify_finish_pair_kernel
+      // kernel gets it from verify_finish_pair_kernel.  With points_done the
+      // point role already ran (launch_verify_points): scalar blocks only.
       const uint32_t nbs = (cnt + kBlock - 1) / kBlock;
+      const uint32_t nblk = nbs + (x.points_done ? 0u : gp.x);
       if (pre_k)
-        hipLaunchKernelGGL(verify_prep_pair_kernel<true>, dim3(nbs + gp.x), dim3(kBlock), 0, stream, sig, msg_or_k, pk,
+        hipLaunchKernelGGL(verify_prep_pair_kernel<true>, dim3(nblk), dim3(kBlock), 0, stream, sig, msg_or_k, pk,
                            base, cnt, policy, pre, nbs);
       else
-        hipLaunchKernelGGL(verify_prep_pair_kernel<false>, dim3(nbs + gp.x), dim3(kBlock), 0, stream, sig, msg_or_k,
+        hipLaunchKernelGGL(verify_prep_pair_kernel<false>, dim3(nblk), dim3(kBlock), 0, stream, sig, msg_or_k,
                            pk, base, cnt, policy, pre, nbs);
     } else if (fused && pre_k)
       hipLaunchKernelGGL(verify_prep_kernel<true>, g1, dim3(kBlock), 0, stream, sig, msg_or_k, pk, base, cnt, policy,
@@ -1318,6 +1347,8 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   const uint32_t csize = S > 1 ? sub : kPreChunk;
   const uint64_t nchunks = ((uint64_t)n + csize - 1) / csize;
   if (S > (uint32_t)nchunks) S = (uint32_t)nchunks;
+  // points_done covers exactly one lane-pair chunk (launch_verify_points)
+  if (x.points_done && (nchunks != 1 || !verify_pair_points(n, policy, x))) return hipErrorInvalidValue;
   hipError_t e;
   if (S > 1) {
     if ((e = hipEventRecord(x.fork, x.streams[0])) != hipSuccess) return e;
