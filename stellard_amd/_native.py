@@ -41,6 +41,7 @@ STL_TUNE_MAIN_QUEUE = 1
 STL_TUNE_STREAMS = 2
 STL_TUNE_CHUNK_LOG2 = 3
 STL_TUNE_BYTE_SHARDS = 4
+STL_TUNE_QUAD = 5
 
 # per-transaction status of the serialized-transaction entry points
 STL_TX_OK = 0

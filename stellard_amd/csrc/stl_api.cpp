@@ -248,6 +248,7 @@ std::atomic<int> g_tune_queue{1};     // main kernel pulls units from a counter
 std::atomic<int> g_tune_streams{2};   // concurrent streams per device-resident call (A/B: DESIGN.md section 8)
 std::atomic<int> g_tune_sub_log2{0};  // log2 signatures per stream chunk; 0 = by batch size (chunk_for)
 std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
+std::atomic<int> g_tune_quad{1};      // smallest chunks' main kernel on eight lanes per signature
 
 // Chunk size of a device-resident call of n signatures over several streams
 // (DESIGN.md section 4): round(n / 2^18) chunks, at least two, of equal size
@@ -472,6 +473,9 @@ uint32_t verify_grid_for(const Device& d, size_t n) {
 // per SIMD at most (a quarter of the resident lanes).
 uint32_t pair_max_lanes(uint32_t grid) { return grid * stl::kBlock / 4; }
 uint32_t pair_max(const Device& d) { return pair_max_lanes(d.grid); }
+// Largest chunk whose main kernel runs on eight lanes per signature: one
+// quad-kernel wave per SIMD at most (STL_TUNE_QUAD 0: never).
+uint32_t quad_max(const Device& d) { return (uint32_t)g_tune_quad.load() * d.grid * stl::kBlock / 16; }
 
 unsigned long long* dev_counters(Device& d);
 const stl::PhaseClock* phase_clock(Device& d);
@@ -490,6 +494,7 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   stl::VerifyExec x;
   x.grid = verify_grid_for(d, n);
   x.pair_max = pair_max(d);
+  x.quad_max = quad_max(d);
   x.wide = static_cast<const uint4*>(d.wide.p);
   x.counters = dev_counters(d);
   x.clock = phase_clock(d);
@@ -1081,6 +1086,7 @@ int stl_debug_tuning(int key, int value) {
       case STL_TUNE_STREAMS: return g_tune_streams.load();
       case STL_TUNE_CHUNK_LOG2: return g_tune_sub_log2.load();
       case STL_TUNE_BYTE_SHARDS: return g_tune_byte_shards.load();
+      case STL_TUNE_QUAD: return g_tune_quad.load();
       default: return STL_EINVAL;
     }
   }
@@ -1100,6 +1106,9 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_BYTE_SHARDS:
       if (value != 0 && value != 1) return STL_EINVAL;
       return g_tune_byte_shards.exchange(value);
+    case STL_TUNE_QUAD:
+      if (value < 0 || value > 4) return STL_EINVAL;
+      return g_tune_quad.exchange(value);
     default:
       return STL_EINVAL;
   }
@@ -1377,6 +1386,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     stl::VerifyExec x;
     x.grid = verify_grid_for(d, cnt);
     x.pair_max = pair_max(d);
+    x.quad_max = quad_max(d);
     x.wide = static_cast<const uint4*>(d.wide.p);
     x.counters = dev_counters(d);
     x.clock = S > 1 ? nullptr : clock;

@@ -96,6 +96,8 @@ struct VerifyExec {
   uint4* ws[kMaxVerifyStreams] = {};    // verify_ws_bytes(grid, dedup) each
   hipEvent_t fork = nullptr;
   hipEvent_t join[kMaxVerifyStreams] = {};
+  uint32_t quad_max = 0;                // lane-pair chunks up to this size run their main kernel on
+                                        // eight lanes per signature (verify_main_quad_kernel); 0: never
   bool points_done = false;             // one lane-pair chunk whose point role already ran
                                         // (launch_verify_points, ordered before this launch)
 };

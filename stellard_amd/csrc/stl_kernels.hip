@@ -630,6 +630,19 @@ struct WideGlobal {
     d[0] = d0;
     d[1] = d1;
   }
+  // the signed row of wide table `which` as a Niels point
+  __device__ void niels(ge_niels& n, int which) const {
+    const uint32_t a = (uint32_t)(d[which] < 0 ? -d[which] : d[which]);
+    const uint4* src = gtab + ((size_t)which * kWideEntries + a) * kWideQuads;
+    uint32_t row[4 * kWideQuads];
+#pragma unroll
+    for (int c = 0; c < kWideQuads; ++c) {
+      const uint4 v = src[c];
+      row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
+    }
+    wide_row_to_niels(n, row);
+    ge_niels_cneg(n, d[which] < 0);
+  }
   __device__ void madd(ge_p1p1& t, const ge_p3& acc, int which) const {
     const uint32_t a = (uint32_t)(d[which] < 0 ? -d[which] : d[which]);
     const uint4* src = gtab + ((size_t)which * kWideEntries + a) * kWideQuads;
@@ -758,6 +771,244 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main
       reinterpret_cast<uint32_t*>(bitmap)[(base + wsig) >> 5] = half;
       if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popc(half));  // accepted (stl_get_stats)
     }
+  }
+}
+
+// ---- four lanes per chain: the smallest batches (verify_main_quad_kernel) ----
+// A chunk this small leaves most SIMDs idle, so its time is one lane's
+// dependent chain, which a lone wave issues at about one mad64 per 5.8 cycles.
+// Here the four products of each group formula (the squarings of a doubling,
+// the products of an addition or of a conversion) run on the four lanes of a
+// quad, one each, and the quad exchanges them by DPP broadcasts: every lane
+// then holds the whole point again.  Role k = lane & 3 computes product k.
+struct QuadRole {
+  bool b0, b1;  // k & 1, k & 2
+};
+
+template <int S>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, S | (S << 2) | (S << 4) | (S << 6), 0xF, 0xF, false);
+}
+
+// o = [a0, a1, a2, a3][role]
+__device__ __forceinline__ void fe_sel4(fe& o, const fe& a0, const fe& a1, const fe& a2, const fe& a3, QuadRole r) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint32_t lo = r.b0 ? a1.v[i] : a0.v[i];
+    const uint32_t hi = r.b0 ? a3.v[i] : a2.v[i];
+    o.v[i] = r.b1 ? hi : lo;
+  }
+}
+
+__device__ __forceinline__ void quad_gather(fe out[4], const fe& p) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    out[0].v[i] = quad_bcast<0>(p.v[i]);
+    out[1].v[i] = quad_bcast<1>(p.v[i]);
+    out[2].v[i] = quad_bcast<2>(p.v[i]);
+    out[3].v[i] = quad_bcast<3>(p.v[i]);
+  }
+}
+
+// out[j] = a_j * b_j on every lane of the quad (same bounds as fe_mul)
+__device__ __forceinline__ void quad_mul4(fe out[4], const fe& a0, const fe& b0, const fe& a1, const fe& b1,
+                                          const fe& a2, const fe& b2, const fe& a3, const fe& b3, QuadRole r) {
+  fe a, b, p;
+  fe_sel4(a, a0, a1, a2, a3, r);
+  fe_sel4(b, b0, b1, b2, b3, r);
+  fe_mul(p, a, b);
+  quad_gather(out, p);
+}
+
+// ge_p2_dbl (non-lazy X): the four squarings on the four lanes
+__device__ __forceinline__ void quad_p2_dbl(ge_p1p1& r, const ge_p2& p, QuadRole q) {
+  fe XpY, in, sq, S[4];
+  fe_add(XpY, p.X, p.Y);     // [2]
+  fe_sel4(in, p.X, p.Y, p.Z, XpY, q);
+  fe_sq(sq, in);
+  quad_gather(S, sq);        // XX, YY, Z^2, A
+  fe ZZ2;
+  fe_add(ZZ2, S[2], S[2]);   // [2]
+  fe_add(r.Y, S[1], S[0]);   // [2]
+  fe_sub_nc<2>(r.Z, S[1], S[0]);  // [3]
+  fe_sub(r.X, S[3], r.Y);    // [1]
+  fe_sub(r.T, ZZ2, r.Z);     // [1]
+}
+
+// ge_p1p1_to_p3 (the p2 conversion is its first three products)
+__device__ __forceinline__ void quad_to_p3(ge_p3& r, const ge_p1p1& t, QuadRole q) {
+  fe O[4];
+  quad_mul4(O, t.X, t.T, t.Y, t.Z, t.Z, t.T, t.X, t.Y, q);
+  r.X = O[0];
+  r.Y = O[1];
+  r.Z = O[2];
+  r.T = O[3];
+}
+
+__device__ __forceinline__ void quad_to_p2(ge_p2& r, const ge_p1p1& t, QuadRole q) {
+  ge_p3 p;
+  quad_to_p3(p, t, q);
+  r.X = p.X;
+  r.Y = p.Y;
+  r.Z = p.Z;
+}
+
+// ge_add_cached
+__device__ __forceinline__ void quad_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& c, QuadRole q) {
+  fe t, t2, O[4];
+  fe_sub_nc<2>(t, p.Y, p.X);  // [3]
+  fe_add(t2, p.Y, p.X);       // [2]
+  quad_mul4(O, t, c.YmX, t2, c.YpX, c.T2d, p.T, p.Z, c.Z, q);
+  fe D;
+  fe_add(D, O[3], O[3]);      // [2]
+  fe_sub_nc<2>(r.X, O[1], O[0]);  // [3]
+  fe_add(r.Y, O[1], O[0]);    // [2]
+  fe_add(r.Z, D, O[2]);       // [3]
+  fe_sub(r.T, D, O[2]);       // [1]
+}
+
+// ge_madd (the fourth lane's product is not used)
+__device__ __forceinline__ void quad_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& n, QuadRole q) {
+  fe t, t2, O[4];
+  fe_sub_nc<2>(t, p.Y, p.X);  // [3]
+  fe_add(t2, p.Y, p.X);       // [2]
+  quad_mul4(O, t, n.ymx, t2, n.ypx, n.xy2d, p.T, p.Z, p.Z, q);
+  fe D;
+  fe_add(D, p.Z, p.Z);        // [2]
+  fe_sub_nc<2>(r.X, O[1], O[0]);  // [3]
+  fe_add(r.Y, O[1], O[0]);    // [2]
+  fe_add(r.Z, D, O[2]);       // [3]
+  fe_sub(r.T, D, O[2]);       // [1]
+}
+
+// verify_phase2_pair_chain on a quad: the same digits, table and wide-row
+// schedule, every group formula spread over the four lanes.  The lane's
+// table (built by each lane of the quad, stored by role 0) is shared by the
+// quad.
+__device__ void quad_chain(ge_p2& out, const HalfState& p, int par, const TableView& tab, const WideGlobal& wide0,
+                           QuadRole q, bool store) {
+  WideGlobal wide = wide0;
+  {
+    ge_p3 P;
+    affine_to_p3(P, par ? p.P2x : p.P1x, par ? p.P2y : p.P1y);
+    if (store) build_cached_table(tab, P);
+  }
+  __syncthreads();  // role 0's stores before the quad's loads (LDS tails, global heads)
+  const int npos = half_positions((int)(p.tops & 0xffu));
+  uint32_t dg[5], ed[4];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) dg[i] = par ? p.ddig[i] : p.cdig[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ed[i] = par ? p.edig[4 + i] : p.edig[i];
+  ge_p3 acc;
+  ge_p2 acc2;
+  ge_p1p1 t;
+  ge_p3_0(acc);
+  ge_p2_0(acc2);
+  uint32_t w = 0, we = 0;
+#pragma unroll 1
+  for (int i = kHalfDigits - 1; i >= 0; --i) {
+    if ((i & 7) == 7) {
+      w = dg[4];
+#pragma unroll
+      for (int m = 4; m > 0; --m) dg[m] = dg[m - 1];
+    }
+    if ((i & 7) == 4 && i < 32) {
+      we = ed[3];
+#pragma unroll
+      for (int m = 3; m > 0; --m) ed[m] = ed[m - 1];
+    }
+    const int d = (int32_t)w >> 28;
+    w <<= 4;
+    const bool bpos = (i & 3) == 0 && i < 32;  // wave-uniform
+    int de = 0;
+    if (bpos) de = (i & 4) ? (int32_t)we >> 16 : (int32_t)(we << 16) >> 16;
+    if (i >= npos) continue;  // wave-uniform
+    ge_cached c;
+    tab.load(d < 0 ? -d : d, c);
+    if (bpos) wide.prefetch(par ? 0 : de, par ? de : 0);
+    if (i != npos - 1) {
+#pragma unroll 1
+      for (int r = 0; r < 3; ++r) {
+        quad_p2_dbl(t, acc2, q);
+        quad_to_p2(acc2, t, q);
+      }
+      quad_p2_dbl(t, acc2, q);
+      quad_to_p3(acc, t, q);
+    }
+    ge_cached_cneg(c, d < 0);
+    quad_add_cached(t, acc, c, q);
+    if (!bpos) {
+      quad_to_p2(acc2, t, q);
+    } else {
+      quad_to_p3(acc, t, q);
+      ge_niels n;
+      wide.niels(n, par);
+      quad_madd(t, acc, n, q);
+      quad_to_p2(acc2, t, q);
+    }
+  }
+  out = acc2;
+}
+
+// Phase 2 for the smallest chunks (8 x 64 x words lanes within the
+// workspace's slots, quad_max in launch_verify): signature j on lanes 8j..8j+7,
+// lanes 8j..8j+3 the [e_lo]B + [c]P1 chain and 8j+4..8j+7 the [e_hi]2^128 B +
+// [d]P2 chain (verify_phase2_pair_chain's split), each on a quad; the chains'
+// sums are exchanged (lane ^ 4) and tested to cancel.  A wave decides 8
+// signatures: one bitmap byte.  Same phase-1 input as the pair kernel.
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_quad_kernel(
+    const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint32_t policy, uint64_t* __restrict__ bitmap,
+    uint64_t* __restrict__ fb_words, uint4* __restrict__ ws, const uint4* __restrict__ wide,
+    unsigned long long* __restrict__ ctr) {
+  // one table per quad: heads in the per-lane slots (slot = global lane / 4),
+  // tails in LDS
+  __shared__ uint4 tails[9][kBlock / 4];
+  const size_t gl = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  TableView tab = TableView::split(ws + (gl >> 2) * kHeadQuads, &tails[0][threadIdx.x >> 2], kIdentityHead,
+                                   kBlock / 4);
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const QuadRole q{(lane & 1u) != 0, (lane & 2u) != 0};
+  const bool role0 = (lane & 3u) == 0;
+  const int par = (int)((lane >> 2) & 1u);
+  const WideGlobal wl{wide, {0, 0}};
+  const uint32_t words = (cnt + 63) >> 6;
+  // every byte of every bitmap word the chunk owns is written (the fallback
+  // kernel ORs into whole words)
+  for (uint32_t tile = blockIdx.x * kBlock; tile < 8u * 64u * words; tile += gridDim.x * kBlock) {
+    const uint32_t t = (tile + threadIdx.x) >> 3;  // signature of this lane octet
+    const bool live = t < cnt;
+    HalfState h;
+    ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
+    {
+      const fe nAx = h.P1x, nAy = h.P1y, nQx = h.P2x, nQy = h.P2y;
+      finish_phase1_points(h, nAx, nAy, nQx, nQy, (h.pad & kPairPointOk) != 0);
+      if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+    }
+    const uint64_t fball = __ballot(live && (h.tops & kHalfFallback) != 0);
+    ge_p2 mine, other;
+    quad_chain(mine, h, par, tab, wl, q, role0);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      other.X.v[i] = (uint32_t)__shfl_xor((int)mine.X.v[i], 4);
+      other.Y.v[i] = (uint32_t)__shfl_xor((int)mine.Y.v[i], 4);
+      other.Z.v[i] = (uint32_t)__shfl_xor((int)mine.Z.v[i], 4);
+    }
+    const bool ok = live && half_state_accepts(h) && pair_sums_cancel(mine, other);
+    const uint64_t ball = __ballot(ok);
+    uint32_t byte = 0, fbyte = 0;  // lane 8j's bits
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      byte |= (uint32_t)((ball >> (8 * b)) & 1u) << b;
+      fbyte |= (uint32_t)((fball >> (8 * b)) & 1u) << b;
+    }
+    const uint32_t wsig = (tile + wave * 64) >> 3;  // first signature of this wave, a multiple of 8
+    if (lane == 0 && (wsig >> 6) < words) {
+      reinterpret_cast<uint8_t*>(fb_words)[wsig >> 3] = (uint8_t)fbyte;
+      reinterpret_cast<uint8_t*>(bitmap)[(base + wsig) >> 3] = (uint8_t)byte;
+      if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popc(byte));  // accepted (stl_get_stats)
+    }
+    __syncthreads();  // the next tile's table stores after every quad's last loads
   }
 }
 
@@ -1307,7 +1558,15 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
     mark(2);
-    if (pair)
+    // the smallest chunks: eight lanes per signature (two per-quad chains),
+    // one table per quad -- 2 x words workgroups, a quarter of their lanes'
+    // slots
+    const uint32_t words = (cnt + 63) / 64;
+    const bool quad = pair && cnt <= x.quad_max && words <= 2 * grid;
+    if (quad)
+      hipLaunchKernelGGL(verify_main_quad_kernel, dim3(2 * words), dim3(kBlock), 0, stream, pre, base, cnt, policy,
+                         bitmap, fb, slots, wide, counters);
+    else if (pair)
       hipLaunchKernelGGL(verify_main_pair_kernel, gp, dim3(kBlock), 0, stream, pre, base, cnt, policy, bitmap, fb,
                          slots, wide, counters);
     else if (!dedup)

@@ -577,6 +577,7 @@ def debug_verify_k_device(sig, k, pk, out_words=None, policy=POLICY_SODIUM_1_0_1
 TUNE_FUSED_PREP, TUNE_MAIN_QUEUE = N.STL_TUNE_FUSED_PREP, N.STL_TUNE_MAIN_QUEUE
 TUNE_STREAMS, TUNE_CHUNK_LOG2 = N.STL_TUNE_STREAMS, N.STL_TUNE_CHUNK_LOG2
 TUNE_BYTE_SHARDS = N.STL_TUNE_BYTE_SHARDS
+TUNE_QUAD = N.STL_TUNE_QUAD
 
 
 def debug_tuning(key, value):
@@ -593,7 +594,7 @@ def execution_settings():
     lib = N.load()
     return {name: lib.stl_debug_tuning(key, -1) for name, key in (
         ("fused_prep", TUNE_FUSED_PREP), ("main_queue", TUNE_MAIN_QUEUE), ("streams", TUNE_STREAMS),
-        ("chunk_log2", TUNE_CHUNK_LOG2))}
+        ("chunk_log2", TUNE_CHUNK_LOG2), ("quad", TUNE_QUAD))}
 
 
 def sign_batch_device(seed, msg, stream=None):

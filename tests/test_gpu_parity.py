@@ -166,14 +166,16 @@ def test_ragged_sizes(stl, golden, n):
     assert np.array_equal(got, golden["expected_sodium_1_0_18"][idx].astype(bool))
 
 
-def test_pair_lanes_same_bits(stl, oracle, torch_cuda):
+@pytest.mark.parametrize("quad", [1, 0])
+def test_pair_lanes_same_bits(stl, oracle, torch_cuda, quad):
     """Batches up to a quarter of the resident lanes run each signature on two lanes
-    (verify_main_pair_kernel); STL_ONE_LANE forces one lane.  Both give the
-    oracle's bits on mutated rows at ragged sizes either side of the switches
-    (the point kernel pairs up to twice the main kernel's limit),
-    on the host and device APIs; the accept counter counts the pair path's
-    bits once.  Pre-filled output words show that every word of the batch is
-    written (bits past n included)."""
+    (verify_main_pair_kernel), the smallest (one wave per SIMD at eight lanes
+    per signature, STL_TUNE_QUAD 1) on lane quads (verify_main_quad_kernel);
+    STL_ONE_LANE forces one lane.  All give the oracle's bits on mutated rows
+    at ragged sizes either side of the switches (the point kernel pairs up to
+    twice the main kernel's limit), on the host and device APIs; the accept
+    counter counts the bits once.  Pre-filled output words show that every
+    word of the batch is written (bits past n included)."""
     torch = torch_cuda
     n = 70000
     sig, msg, pk = _gpu_signed(stl, torch, n, 4711)
@@ -181,7 +183,15 @@ def test_pair_lanes_same_bits(stl, oracle, torch_cuda):
     s, m, p = _mutate(sig.cpu().numpy(), msg.cpu().numpy(), pk.cpu().numpy(), rng)
     exp = oracle.verify_batch(s, m, p, threads=16)
     ds, dm, dp = (torch.from_numpy(a).cuda() for a in (s, m, p))
-    for k in (1, 31, 33, 95, 4097, 32767, 32768, 32769, 49153, 65536, 65537, 70000):
+    old = stl.debug_tuning(stl.TUNE_QUAD, quad)
+    try:
+        _pair_sizes(stl, torch, s, m, p, ds, dm, dp, exp)
+    finally:
+        stl.debug_tuning(stl.TUNE_QUAD, old)
+
+
+def _pair_sizes(stl, torch, s, m, p, ds, dm, dp, exp):
+    for k in (1, 31, 33, 95, 4097, 8191, 8192, 8193, 32767, 32768, 32769, 49153, 65536, 65537, 70000):
         two = stl.verify_batch(s[:k], m[:k], p[:k])
         one = stl.verify_batch(s[:k], m[:k], p[:k], policy=stl.ONE_LANE)
         assert np.array_equal(two, exp[:k]), (k, np.nonzero(two != exp[:k])[0][:10])

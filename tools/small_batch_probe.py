@@ -23,6 +23,8 @@ def main():
     from stellard_amd import verify as V
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     V.init()
+    if os.environ.get("PROBE_QUAD"):  # A/B of the quad main kernel (STL_TUNE_QUAD)
+        V.debug_tuning(V.TUNE_QUAD, int(os.environ["PROBE_QUAD"]))
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream()
     lp = datasets.ledger_plan()
@@ -34,7 +36,8 @@ def main():
     pk, sig = V.sign_batch_device(seeds, msgs)
     torch.cuda.synchronize()
     out = {}
-    for n in (1000, 4000, 8000, 19000, 40000):
+    sizes = [int(x) for x in os.environ.get("PROBE_SIZES", "1000,4000,8000,19000,40000").split(",")]
+    for n in sizes:
         w = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
         m = torch.empty((n, 32), dtype=torch.uint8, device=dev)
         sl = slice(4096, 4096 + n)
