@@ -74,8 +74,8 @@ extern "C" {
  * wide key tables), allocated once per device for the host batch API and once
  * per (device, stream) -- per library stream too -- for the device-resident
  * API; does not pay when keys are all distinct.  Chunks small enough for lane
- * pairs (STL_ONE_LANE below) run on pairs instead: latency-bound there, the
- * pairs are faster. */
+ * pairs or quads (STL_ONE_LANE below) run on them instead: latency-bound
+ * there, the pairs and quads are faster. */
 #define STL_DEDUP_KEYS 0x8u
 /* The host batch calls (stl_ed25519_verify_batch, stl_tx_verify_batch, the
  * blob calls) choose STL_DEDUP_KEYS by themselves for every 64K-row chunk in
@@ -90,8 +90,10 @@ extern "C" {
 /* Small chunks run each signature on two lanes, which ends a launch that
  * cannot fill the device sooner: the main kernel up to
  * a quarter of the device's resident lanes (one pair wave per SIMD; 32,768
- * signatures on 256 CUs), the point decoding up to half of them.  Same accept
- * bits; this flag turns it off (A/B and tests). */
+ * signatures on 256 CUs), on eight lanes (two lane quads) up to one quad wave
+ * per SIMD (8,192 signatures; STL_TUNE_QUAD), the point decoding on pairs up
+ * to half of them.  Same accept bits; this flag turns both off (A/B and
+ * tests). */
 #define STL_ONE_LANE 0x10u
 /* TEST-ONLY: the raw crypto_sign_verify_detached predicate of the selected
  * policy, without stellard's S < L -- what RippleAddress_test expects of the
@@ -157,8 +159,9 @@ const char *stl_strerror(int rc);
  * from a reject by the caller (rc < -1).  STL_EINVAL (a NULL pointer) is
  * returned either way; a message longer than 2^32 - 1 bytes is STL_EINVAL
  * without a fallback and the fallback's answer (&& S < L) with one.
- * LATENCY: a signature is one GPU lane pair, so a call is latency-bound: 489 us
- * per call on MI355X against libsodium's 32 us, and concurrent calls
+ * LATENCY: a signature's chain runs on eight GPU lanes (two lane quads), so a
+ * call is latency-bound: 332 us per call on MI355X against libsodium's 31 us
+ * (round 4; 489 us on lane pairs in round 2), and concurrent calls
  * serialise on the device (tools/latency.py).
  * Callers that verify one signature at a time (stellard's JobQueue workers)
  * keep libsodium, or submit through stl_batcher_* when many requests are in
