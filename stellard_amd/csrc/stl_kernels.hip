@@ -881,17 +881,50 @@ __device__ __forceinline__ void quad_madd(ge_p1p1& r, const ge_p3& p, const ge_n
   fe_sub(r.T, D, O[2]);       // [1]
 }
 
+// build_cached_table on a quad: entries 2..8 from quad doublings / madds
+// (same points; the doubling of the affine P with Z = 1 is ge_affine_dbl's
+// arithmetic), the cached conversions on every lane, the stores by `store`.
+__device__ void quad_build_table(const TableView& tab, const ge_p3& P, QuadRole q, bool store) {
+  ge_cached c1, c;
+  ge_cached_0(c);
+  if (store) tab.store(0, c);
+  ge_p3_to_cached(c1, P);
+  if (store) tab.store(1, c1);
+  ge_niels n1;
+  n1.ypx = c1.YpX;
+  n1.ymx = c1.YmX;
+  n1.xy2d = c1.T2d;
+  ge_p1p1 t;
+  ge_p3 p3;
+  {
+    ge_p2 P2;
+    P2.X = P.X;
+    P2.Y = P.Y;
+    P2.Z = P.Z;
+    quad_p2_dbl(t, P2, q);
+  }
+  quad_to_p3(p3, t, q);
+  ge_p3_to_cached(c, p3);
+  if (store) tab.store(2, c);
+#pragma unroll 1
+  for (int e = 3; e <= 8; ++e) {
+    quad_madd(t, p3, n1, q);
+    quad_to_p3(p3, t, q);
+    ge_p3_to_cached(c, p3);
+    if (store) tab.store(e, c);
+  }
+}
+
 // verify_phase2_pair_chain on a quad: the same digits, table and wide-row
-// schedule, every group formula spread over the four lanes.  The lane's
-// table (built by each lane of the quad, stored by role 0) is shared by the
-// quad.
+// schedule, every group formula spread over the four lanes.  One table per
+// quad (built by the quad, stored by role 0).
 __device__ void quad_chain(ge_p2& out, const HalfState& p, int par, const TableView& tab, const WideGlobal& wide0,
                            QuadRole q, bool store) {
   WideGlobal wide = wide0;
   {
     ge_p3 P;
     affine_to_p3(P, par ? p.P2x : p.P1x, par ? p.P2y : p.P1y);
-    if (store) build_cached_table(tab, P);
+    quad_build_table(tab, P, q, store);
   }
   __syncthreads();  // role 0's stores before the quad's loads (LDS tails, global heads)
   const int npos = half_positions((int)(p.tops & 0xffu));
