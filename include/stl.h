@@ -407,10 +407,11 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
 #define STL_TUNE_BYTE_SHARDS 4 /* 1: host preimage / blob batches take the byte-balanced shard path even
                                   as one shard (test hook: runs the grouped-gather placement and
                                   rank 0's device copy on one GPU under STL_CFG_RCCL_GATHER) */
-#define STL_TUNE_QUAD 5        /* 1 (default): chunks of at most one wave per SIMD at eight lanes per
-                                  signature run the main kernel on lane quads (each group formula's
-                                  products spread over four lanes); 0: lane pairs; 2..4: up to that
-                                  many quad waves per SIMD (A/B only: slower than pairs there) */
+#define STL_TUNE_QUAD 5        /* lane groups for the smallest chunks' main kernel, bits: 1 = chunks of
+                                  at most one wave per SIMD at eight lanes per signature run on lane
+                                  quads (each group formula's four products one per lane), 2 = the
+                                  next ones up to one wave per SIMD at four lanes on lane duos (two
+                                  products per lane); 3 (default) both, 0 lane pairs only */
 int stl_debug_tuning(int key, int value);
 
 /* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;

@@ -248,7 +248,7 @@ std::atomic<int> g_tune_queue{1};     // main kernel pulls units from a counter
 std::atomic<int> g_tune_streams{2};   // concurrent streams per device-resident call (A/B: DESIGN.md section 8)
 std::atomic<int> g_tune_sub_log2{0};  // log2 signatures per stream chunk; 0 = by batch size (chunk_for)
 std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
-std::atomic<int> g_tune_quad{1};      // smallest chunks' main kernel on eight lanes per signature
+std::atomic<int> g_tune_quad{3};      // smallest chunks' main kernel on lane groups: bit 0 quads, bit 1 duos
 
 // Chunk size of a device-resident call of n signatures over several streams
 // (DESIGN.md section 4): round(n / 2^18) chunks, at least two, of equal size
@@ -473,9 +473,11 @@ uint32_t verify_grid_for(const Device& d, size_t n) {
 // per SIMD at most (a quarter of the resident lanes).
 uint32_t pair_max_lanes(uint32_t grid) { return grid * stl::kBlock / 4; }
 uint32_t pair_max(const Device& d) { return pair_max_lanes(d.grid); }
-// Largest chunk whose main kernel runs on eight lanes per signature: one
-// quad-kernel wave per SIMD at most (STL_TUNE_QUAD 0: never).
-uint32_t quad_max(const Device& d) { return (uint32_t)g_tune_quad.load() * d.grid * stl::kBlock / 16; }
+// Largest chunks whose main kernel runs on eight (quad_max) or four (duo_max)
+// lanes per signature: one such wave per SIMD at most (a second one per SIMD
+// measured slower than lane pairs; STL_TUNE_QUAD bits 0 / 1 turn them on).
+uint32_t quad_max(const Device& d) { return (g_tune_quad.load() & 1) ? d.grid * stl::kBlock / 16 : 0u; }
+uint32_t duo_max(const Device& d) { return (g_tune_quad.load() & 2) ? d.grid * stl::kBlock / 8 : 0u; }
 
 unsigned long long* dev_counters(Device& d);
 const stl::PhaseClock* phase_clock(Device& d);
@@ -495,6 +497,7 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   x.grid = verify_grid_for(d, n);
   x.pair_max = pair_max(d);
   x.quad_max = quad_max(d);
+  x.duo_max = duo_max(d);
   x.wide = static_cast<const uint4*>(d.wide.p);
   x.counters = dev_counters(d);
   x.clock = phase_clock(d);
@@ -1107,7 +1110,7 @@ int stl_debug_tuning(int key, int value) {
       if (value != 0 && value != 1) return STL_EINVAL;
       return g_tune_byte_shards.exchange(value);
     case STL_TUNE_QUAD:
-      if (value < 0 || value > 4) return STL_EINVAL;
+      if (value < 0 || value > 3) return STL_EINVAL;
       return g_tune_quad.exchange(value);
     default:
       return STL_EINVAL;
@@ -1387,6 +1390,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     x.grid = verify_grid_for(d, cnt);
     x.pair_max = pair_max(d);
     x.quad_max = quad_max(d);
+    x.duo_max = duo_max(d);
     x.wide = static_cast<const uint4*>(d.wide.p);
     x.counters = dev_counters(d);
     x.clock = S > 1 ? nullptr : clock;

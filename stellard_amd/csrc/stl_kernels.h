@@ -97,7 +97,8 @@ struct VerifyExec {
   hipEvent_t fork = nullptr;
   hipEvent_t join[kMaxVerifyStreams] = {};
   uint32_t quad_max = 0;                // lane-pair chunks up to this size run their main kernel on
-                                        // eight lanes per signature (verify_main_quad_kernel); 0: never
+                                        // eight lanes per signature (verify_main_group_kernel<4>),
+  uint32_t duo_max = 0;                 // up to this size on four (verify_main_group_kernel<2>); 0: never
   bool points_done = false;             // one lane-pair chunk whose point role already ran
                                         // (launch_verify_points, ordered before this launch)
 };

@@ -774,15 +774,17 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main
   }
 }
 
-// ---- four lanes per chain: the smallest batches (verify_main_quad_kernel) ----
+// ---- lane groups per chain: the smallest batches (verify_main_group_kernel) ----
 // A chunk this small leaves most SIMDs idle, so its time is one lane's
 // dependent chain, which a lone wave issues at about one mad64 per 5.8 cycles.
 // Here the four products of each group formula (the squarings of a doubling,
-// the products of an addition or of a conversion) run on the four lanes of a
-// quad, one each, and the quad exchanges them by DPP broadcasts: every lane
-// then holds the whole point again.  Role k = lane & 3 computes product k.
-struct QuadRole {
-  bool b0, b1;  // k & 1, k & 2
+// the products of an addition or of a conversion) are spread over a group of
+// G lanes -- G = 4 (a quad: one product per lane, four DPP quad broadcasts)
+// or G = 2 (a duo: two interleaved products per lane, one DPP pair swap) --
+// and every lane then holds the whole point again.  Role bits b0 = lane & 1,
+// b1 = lane & 2.
+struct GroupRole {
+  bool b0, b1;
 };
 
 template <int S>
@@ -790,8 +792,13 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, S | (S << 2) | (S << 4) | (S << 6), 0xF, 0xF, false);
 }
 
+__device__ __forceinline__ void fe_sel2(fe& o, const fe& a0, const fe& a1, bool b) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) o.v[i] = b ? a1.v[i] : a0.v[i];
+}
+
 // o = [a0, a1, a2, a3][role]
-__device__ __forceinline__ void fe_sel4(fe& o, const fe& a0, const fe& a1, const fe& a2, const fe& a3, QuadRole r) {
+__device__ __forceinline__ void fe_sel4(fe& o, const fe& a0, const fe& a1, const fe& a2, const fe& a3, GroupRole r) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const uint32_t lo = r.b0 ? a1.v[i] : a0.v[i];
@@ -810,23 +817,62 @@ __device__ __forceinline__ void quad_gather(fe out[4], const fe& p) {
   }
 }
 
-// out[j] = a_j * b_j on every lane of the quad (same bounds as fe_mul)
-__device__ __forceinline__ void quad_mul4(fe out[4], const fe& a0, const fe& b0, const fe& a1, const fe& b1,
-                                          const fe& a2, const fe& b2, const fe& a3, const fe& b3, QuadRole r) {
-  fe a, b, p;
-  fe_sel4(a, a0, a1, a2, a3, r);
-  fe_sel4(b, b0, b1, b2, b3, r);
-  fe_mul(p, a, b);
-  quad_gather(out, p);
+// duo: this lane's products p0, p1 are products 2*b0 and 2*b0 + 1
+__device__ __forceinline__ void duo_gather(fe out[4], const fe& p0, const fe& p1, bool b0) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint32_t q0 = pair_swap(p0.v[i]), q1 = pair_swap(p1.v[i]);
+    out[0].v[i] = b0 ? q0 : p0.v[i];
+    out[1].v[i] = b0 ? q1 : p1.v[i];
+    out[2].v[i] = b0 ? p0.v[i] : q0;
+    out[3].v[i] = b0 ? p1.v[i] : q1;
+  }
 }
 
-// ge_p2_dbl (non-lazy X): the four squarings on the four lanes
-__device__ __forceinline__ void quad_p2_dbl(ge_p1p1& r, const ge_p2& p, QuadRole q) {
-  fe XpY, in, sq, S[4];
+// out[j] = a_j * b_j on every lane of the group (same bounds as fe_mul)
+template <int G>
+__device__ __forceinline__ void group_mul4(fe out[4], const fe& a0, const fe& b0, const fe& a1, const fe& b1,
+                                           const fe& a2, const fe& b2, const fe& a3, const fe& b3, GroupRole r) {
+  if (G == 4) {
+    fe a, b, p;
+    fe_sel4(a, a0, a1, a2, a3, r);
+    fe_sel4(b, b0, b1, b2, b3, r);
+    fe_mul(p, a, b);
+    quad_gather(out, p);
+  } else {
+    fe x0, y0, x1, y1, p0, p1;
+    fe_sel2(x0, a0, a2, r.b0);
+    fe_sel2(y0, b0, b2, r.b0);
+    fe_sel2(x1, a1, a3, r.b0);
+    fe_sel2(y1, b1, b3, r.b0);
+    fe_mul2(p0, x0, y0, p1, x1, y1);
+    duo_gather(out, p0, p1, r.b0);
+  }
+}
+
+template <int G>
+__device__ __forceinline__ void group_sq4(fe out[4], const fe& a0, const fe& a1, const fe& a2, const fe& a3,
+                                          GroupRole r) {
+  if (G == 4) {
+    fe a, p;
+    fe_sel4(a, a0, a1, a2, a3, r);
+    fe_sq(p, a);
+    quad_gather(out, p);
+  } else {
+    fe x0, x1, p0, p1;
+    fe_sel2(x0, a0, a2, r.b0);
+    fe_sel2(x1, a1, a3, r.b0);
+    fe_sq2(p0, x0, p1, x1);
+    duo_gather(out, p0, p1, r.b0);
+  }
+}
+
+// ge_p2_dbl (non-lazy X): the four squarings spread over the group
+template <int G>
+__device__ __forceinline__ void group_p2_dbl(ge_p1p1& r, const ge_p2& p, GroupRole q) {
+  fe XpY, S[4];
   fe_add(XpY, p.X, p.Y);     // [2]
-  fe_sel4(in, p.X, p.Y, p.Z, XpY, q);
-  fe_sq(sq, in);
-  quad_gather(S, sq);        // XX, YY, Z^2, A
+  group_sq4<G>(S, p.X, p.Y, p.Z, XpY, q);  // XX, YY, Z^2, A
   fe ZZ2;
   fe_add(ZZ2, S[2], S[2]);   // [2]
   fe_add(r.Y, S[1], S[0]);   // [2]
@@ -836,29 +882,32 @@ __device__ __forceinline__ void quad_p2_dbl(ge_p1p1& r, const ge_p2& p, QuadRole
 }
 
 // ge_p1p1_to_p3 (the p2 conversion is its first three products)
-__device__ __forceinline__ void quad_to_p3(ge_p3& r, const ge_p1p1& t, QuadRole q) {
+template <int G>
+__device__ __forceinline__ void group_to_p3(ge_p3& r, const ge_p1p1& t, GroupRole q) {
   fe O[4];
-  quad_mul4(O, t.X, t.T, t.Y, t.Z, t.Z, t.T, t.X, t.Y, q);
+  group_mul4<G>(O, t.X, t.T, t.Y, t.Z, t.Z, t.T, t.X, t.Y, q);
   r.X = O[0];
   r.Y = O[1];
   r.Z = O[2];
   r.T = O[3];
 }
 
-__device__ __forceinline__ void quad_to_p2(ge_p2& r, const ge_p1p1& t, QuadRole q) {
+template <int G>
+__device__ __forceinline__ void group_to_p2(ge_p2& r, const ge_p1p1& t, GroupRole q) {
   ge_p3 p;
-  quad_to_p3(p, t, q);
+  group_to_p3<G>(p, t, q);
   r.X = p.X;
   r.Y = p.Y;
   r.Z = p.Z;
 }
 
 // ge_add_cached
-__device__ __forceinline__ void quad_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& c, QuadRole q) {
+template <int G>
+__device__ __forceinline__ void group_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& c, GroupRole q) {
   fe t, t2, O[4];
   fe_sub_nc<2>(t, p.Y, p.X);  // [3]
   fe_add(t2, p.Y, p.X);       // [2]
-  quad_mul4(O, t, c.YmX, t2, c.YpX, c.T2d, p.T, p.Z, c.Z, q);
+  group_mul4<G>(O, t, c.YmX, t2, c.YpX, c.T2d, p.T, p.Z, c.Z, q);
   fe D;
   fe_add(D, O[3], O[3]);      // [2]
   fe_sub_nc<2>(r.X, O[1], O[0]);  // [3]
@@ -867,12 +916,13 @@ __device__ __forceinline__ void quad_add_cached(ge_p1p1& r, const ge_p3& p, cons
   fe_sub(r.T, D, O[2]);       // [1]
 }
 
-// ge_madd (the fourth lane's product is not used)
-__device__ __forceinline__ void quad_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& n, QuadRole q) {
+// ge_madd (the fourth product is not used)
+template <int G>
+__device__ __forceinline__ void group_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& n, GroupRole q) {
   fe t, t2, O[4];
   fe_sub_nc<2>(t, p.Y, p.X);  // [3]
   fe_add(t2, p.Y, p.X);       // [2]
-  quad_mul4(O, t, n.ymx, t2, n.ypx, n.xy2d, p.T, p.Z, p.Z, q);
+  group_mul4<G>(O, t, n.ymx, t2, n.ypx, n.xy2d, p.T, p.Z, p.Z, q);
   fe D;
   fe_add(D, p.Z, p.Z);        // [2]
   fe_sub_nc<2>(r.X, O[1], O[0]);  // [3]
@@ -881,10 +931,11 @@ __device__ __forceinline__ void quad_madd(ge_p1p1& r, const ge_p3& p, const ge_n
   fe_sub(r.T, D, O[2]);       // [1]
 }
 
-// build_cached_table on a quad: entries 2..8 from quad doublings / madds
+// build_cached_table on a group: entries 2..8 from group doublings / madds
 // (same points; the doubling of the affine P with Z = 1 is ge_affine_dbl's
 // arithmetic), the cached conversions on every lane, the stores by `store`.
-__device__ void quad_build_table(const TableView& tab, const ge_p3& P, QuadRole q, bool store) {
+template <int G>
+__device__ void group_build_table(const TableView& tab, const ge_p3& P, GroupRole q, bool store) {
   ge_cached c1, c;
   ge_cached_0(c);
   if (store) tab.store(0, c);
@@ -901,32 +952,33 @@ __device__ void quad_build_table(const TableView& tab, const ge_p3& P, QuadRole 
     P2.X = P.X;
     P2.Y = P.Y;
     P2.Z = P.Z;
-    quad_p2_dbl(t, P2, q);
+    group_p2_dbl<G>(t, P2, q);
   }
-  quad_to_p3(p3, t, q);
+  group_to_p3<G>(p3, t, q);
   ge_p3_to_cached(c, p3);
   if (store) tab.store(2, c);
 #pragma unroll 1
   for (int e = 3; e <= 8; ++e) {
-    quad_madd(t, p3, n1, q);
-    quad_to_p3(p3, t, q);
+    group_madd<G>(t, p3, n1, q);
+    group_to_p3<G>(p3, t, q);
     ge_p3_to_cached(c, p3);
     if (store) tab.store(e, c);
   }
 }
 
-// verify_phase2_pair_chain on a quad: the same digits, table and wide-row
-// schedule, every group formula spread over the four lanes.  One table per
-// quad (built by the quad, stored by role 0).
-__device__ void quad_chain(ge_p2& out, const HalfState& p, int par, const TableView& tab, const WideGlobal& wide0,
-                           QuadRole q, bool store) {
+// verify_phase2_pair_chain on a group: the same digits, table and wide-row
+// schedule, every group formula spread over the G lanes.  One table per
+// group (built by the group, stored by its role-0 lane).
+template <int G>
+__device__ void group_chain(ge_p2& out, const HalfState& p, int par, const TableView& tab, const WideGlobal& wide0,
+                            GroupRole q, bool store) {
   WideGlobal wide = wide0;
   {
     ge_p3 P;
     affine_to_p3(P, par ? p.P2x : p.P1x, par ? p.P2y : p.P1y);
-    quad_build_table(tab, P, q, store);
+    group_build_table<G>(tab, P, q, store);
   }
-  __syncthreads();  // role 0's stores before the quad's loads (LDS tails, global heads)
+  __syncthreads();  // role 0's stores before the group's loads (LDS tails, global heads)
   const int npos = half_positions((int)(p.tops & 0xffu));
   uint32_t dg[5], ed[4];
 #pragma unroll
@@ -963,53 +1015,58 @@ __device__ void quad_chain(ge_p2& out, const HalfState& p, int par, const TableV
     if (i != npos - 1) {
 #pragma unroll 1
       for (int r = 0; r < 3; ++r) {
-        quad_p2_dbl(t, acc2, q);
-        quad_to_p2(acc2, t, q);
+        group_p2_dbl<G>(t, acc2, q);
+        group_to_p2<G>(acc2, t, q);
       }
-      quad_p2_dbl(t, acc2, q);
-      quad_to_p3(acc, t, q);
+      group_p2_dbl<G>(t, acc2, q);
+      group_to_p3<G>(acc, t, q);
     }
     ge_cached_cneg(c, d < 0);
-    quad_add_cached(t, acc, c, q);
+    group_add_cached<G>(t, acc, c, q);
     if (!bpos) {
-      quad_to_p2(acc2, t, q);
+      group_to_p2<G>(acc2, t, q);
     } else {
-      quad_to_p3(acc, t, q);
+      group_to_p3<G>(acc, t, q);
       ge_niels n;
       wide.niels(n, par);
-      quad_madd(t, acc, n, q);
-      quad_to_p2(acc2, t, q);
+      group_madd<G>(t, acc, n, q);
+      group_to_p2<G>(acc2, t, q);
     }
   }
   out = acc2;
 }
 
-// Phase 2 for the smallest chunks (8 x 64 x words lanes within the
-// workspace's slots, quad_max in launch_verify): signature j on lanes 8j..8j+7,
-// lanes 8j..8j+3 the [e_lo]B + [c]P1 chain and 8j+4..8j+7 the [e_hi]2^128 B +
-// [d]P2 chain (verify_phase2_pair_chain's split), each on a quad; the chains'
-// sums are exchanged (lane ^ 4) and tested to cancel.  A wave decides 8
-// signatures: one bitmap byte.  Same phase-1 input as the pair kernel.
-__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_quad_kernel(
+// Phase 2 for the smallest chunks (one group wave per SIMD at most:
+// quad_max / duo_max in launch_verify): signature j on lanes 2Gj..2Gj+2G-1,
+// the first G lanes the [e_lo]B + [c]P1 chain and the next G the
+// [e_hi]2^128 B + [d]P2 chain (verify_phase2_pair_chain's split); the
+// chains' sums are exchanged (lane ^ G) and tested to cancel.  A wave decides
+// 64 / 2G signatures: a bitmap byte (G = 4) or half-word (G = 2).  Same
+// phase-1 input as the pair kernel.
+template <int G>
+__global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main_group_kernel(
     const uint4* __restrict__ pre, uint32_t base, uint32_t cnt, uint32_t policy, uint64_t* __restrict__ bitmap,
     uint64_t* __restrict__ fb_words, uint4* __restrict__ ws, const uint4* __restrict__ wide,
     unsigned long long* __restrict__ ctr) {
-  // one table per quad: heads in the per-lane slots (slot = global lane / 4),
+  static_assert(G == 2 || G == 4, "group size");
+  constexpr uint32_t kLanes = 2 * G;          // lanes per signature
+  constexpr uint32_t kSigsPerWave = 64 / kLanes;
+  // one table per group: heads in the per-lane slots (slot = global lane / G),
   // tails in LDS
-  __shared__ uint4 tails[9][kBlock / 4];
+  __shared__ uint4 tails[9][kBlock / G];
   const size_t gl = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  TableView tab = TableView::split(ws + (gl >> 2) * kHeadQuads, &tails[0][threadIdx.x >> 2], kIdentityHead,
-                                   kBlock / 4);
+  TableView tab = TableView::split(ws + (gl / G) * kHeadQuads, &tails[0][threadIdx.x / G], kIdentityHead,
+                                   kBlock / G);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const QuadRole q{(lane & 1u) != 0, (lane & 2u) != 0};
-  const bool role0 = (lane & 3u) == 0;
-  const int par = (int)((lane >> 2) & 1u);
+  const GroupRole q{(lane & 1u) != 0, (lane & 2u) != 0};
+  const bool role0 = (lane & (G - 1)) == 0;
+  const int par = (int)((lane / G) & 1u);
   const WideGlobal wl{wide, {0, 0}};
   const uint32_t words = (cnt + 63) >> 6;
-  // every byte of every bitmap word the chunk owns is written (the fallback
+  // every bit of every bitmap word the chunk owns is written (the fallback
   // kernel ORs into whole words)
-  for (uint32_t tile = blockIdx.x * kBlock; tile < 8u * 64u * words; tile += gridDim.x * kBlock) {
-    const uint32_t t = (tile + threadIdx.x) >> 3;  // signature of this lane octet
+  for (uint32_t tile = blockIdx.x * kBlock; tile < kLanes * 64u * words; tile += gridDim.x * kBlock) {
+    const uint32_t t = (tile + threadIdx.x) / kLanes;  // signature of this lane's group pair
     const bool live = t < cnt;
     HalfState h;
     ld_state_words<14>(h, pre + (size_t)(live ? t : cnt - 1) * 14);
@@ -1020,28 +1077,33 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main
     }
     const uint64_t fball = __ballot(live && (h.tops & kHalfFallback) != 0);
     ge_p2 mine, other;
-    quad_chain(mine, h, par, tab, wl, q, role0);
+    group_chain<G>(mine, h, par, tab, wl, q, role0);
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-      other.X.v[i] = (uint32_t)__shfl_xor((int)mine.X.v[i], 4);
-      other.Y.v[i] = (uint32_t)__shfl_xor((int)mine.Y.v[i], 4);
-      other.Z.v[i] = (uint32_t)__shfl_xor((int)mine.Z.v[i], 4);
+      other.X.v[i] = (uint32_t)__shfl_xor((int)mine.X.v[i], G);
+      other.Y.v[i] = (uint32_t)__shfl_xor((int)mine.Y.v[i], G);
+      other.Z.v[i] = (uint32_t)__shfl_xor((int)mine.Z.v[i], G);
     }
     const bool ok = live && half_state_accepts(h) && pair_sums_cancel(mine, other);
     const uint64_t ball = __ballot(ok);
-    uint32_t byte = 0, fbyte = 0;  // lane 8j's bits
+    uint32_t bits = 0, fbits = 0;  // the first lane of each signature's lanes
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      byte |= (uint32_t)((ball >> (8 * b)) & 1u) << b;
-      fbyte |= (uint32_t)((fball >> (8 * b)) & 1u) << b;
+    for (uint32_t b = 0; b < kSigsPerWave; ++b) {
+      bits |= (uint32_t)((ball >> (kLanes * b)) & 1u) << b;
+      fbits |= (uint32_t)((fball >> (kLanes * b)) & 1u) << b;
     }
-    const uint32_t wsig = (tile + wave * 64) >> 3;  // first signature of this wave, a multiple of 8
+    const uint32_t wsig = (tile + wave * 64) / kLanes;  // first signature of this wave
     if (lane == 0 && (wsig >> 6) < words) {
-      reinterpret_cast<uint8_t*>(fb_words)[wsig >> 3] = (uint8_t)fbyte;
-      reinterpret_cast<uint8_t*>(bitmap)[(base + wsig) >> 3] = (uint8_t)byte;
-      if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popc(byte));  // accepted (stl_get_stats)
+      if (G == 4) {
+        reinterpret_cast<uint8_t*>(fb_words)[wsig >> 3] = (uint8_t)fbits;
+        reinterpret_cast<uint8_t*>(bitmap)[(base + wsig) >> 3] = (uint8_t)bits;
+      } else {
+        reinterpret_cast<uint16_t*>(fb_words)[wsig >> 4] = (uint16_t)fbits;
+        reinterpret_cast<uint16_t*>(bitmap)[(base + wsig) >> 4] = (uint16_t)bits;
+      }
+      if (ctr) atomicAdd(&ctr[0], (unsigned long long)__popc(bits));  // accepted (stl_get_stats)
     }
-    __syncthreads();  // the next tile's table stores after every quad's last loads
+    __syncthreads();  // the next tile's table stores after every group's last loads
   }
 }
 
@@ -1591,13 +1653,16 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
     mark(2);
-    // the smallest chunks: eight lanes per signature (two per-quad chains),
-    // one table per quad -- 2 x words workgroups, a quarter of their lanes'
-    // slots
+    // lane groups: G lanes per chain, 2G per signature, one table per group:
+    // G * words / 2 workgroups, whose slots (one per G lanes) fit the
+    // workspace when words <= 2 * grid
     const uint32_t words = (cnt + 63) / 64;
-    const bool quad = pair && cnt <= x.quad_max && words <= 2 * grid;
-    if (quad)
-      hipLaunchKernelGGL(verify_main_quad_kernel, dim3(2 * words), dim3(kBlock), 0, stream, pre, base, cnt, policy,
+    const bool fits = pair && words <= 2 * grid;
+    if (fits && cnt <= x.quad_max)
+      hipLaunchKernelGGL(verify_main_group_kernel<4>, dim3(2 * words), dim3(kBlock), 0, stream, pre, base, cnt, policy,
+                         bitmap, fb, slots, wide, counters);
+    else if (fits && cnt <= x.duo_max)
+      hipLaunchKernelGGL(verify_main_group_kernel<2>, dim3(words), dim3(kBlock), 0, stream, pre, base, cnt, policy,
                          bitmap, fb, slots, wide, counters);
     else if (pair)
       hipLaunchKernelGGL(verify_main_pair_kernel, gp, dim3(kBlock), 0, stream, pre, base, cnt, policy, bitmap, fb,

@@ -193,7 +193,7 @@ def test_tuning_rejects_bad_values(stl):
     from stellard_amd import _native as N
     lib = N.load()
     for key, bad in ((stl.TUNE_FUSED_PREP, 2), (stl.TUNE_FUSED_PREP, 3), (stl.TUNE_FUSED_PREP, -2), (stl.TUNE_MAIN_QUEUE, -2), (stl.TUNE_STREAMS, 0),
-                     (stl.TUNE_STREAMS, 5), (stl.TUNE_CHUNK_LOG2, 14), (stl.TUNE_CHUNK_LOG2, 21), (stl.TUNE_QUAD, 5), (stl.TUNE_QUAD, -2), (99, 1)):
+                     (stl.TUNE_STREAMS, 5), (stl.TUNE_CHUNK_LOG2, 14), (stl.TUNE_CHUNK_LOG2, 21), (stl.TUNE_QUAD, 4), (stl.TUNE_QUAD, -2), (99, 1)):
         assert lib.stl_debug_tuning(key, bad) == N.STL_EINVAL, (key, bad)
     assert stl.execution_settings()["streams"] in (1, 2, 3, 4)
 

@@ -166,7 +166,7 @@ def test_ragged_sizes(stl, golden, n):
     assert np.array_equal(got, golden["expected_sodium_1_0_18"][idx].astype(bool))
 
 
-@pytest.mark.parametrize("quad", [1, 0])
+@pytest.mark.parametrize("quad", [3, 1, 0])
 def test_pair_lanes_same_bits(stl, oracle, torch_cuda, quad):
     """Batches up to a quarter of the resident lanes run each signature on two lanes
     (verify_main_pair_kernel), the smallest (one wave per SIMD at eight lanes
@@ -191,7 +191,8 @@ def test_pair_lanes_same_bits(stl, oracle, torch_cuda, quad):
 
 
 def _pair_sizes(stl, torch, s, m, p, ds, dm, dp, exp):
-    for k in (1, 31, 33, 95, 4097, 8191, 8192, 8193, 32767, 32768, 32769, 49153, 65536, 65537, 70000):
+    for k in (1, 31, 33, 95, 4097, 8191, 8192, 8193, 12000, 16384, 16385, 32767, 32768, 32769, 49153, 65536, 65537,
+              70000):
         two = stl.verify_batch(s[:k], m[:k], p[:k])
         one = stl.verify_batch(s[:k], m[:k], p[:k], policy=stl.ONE_LANE)
         assert np.array_equal(two, exp[:k]), (k, np.nonzero(two != exp[:k])[0][:10])
