@@ -91,8 +91,9 @@ extern "C" {
  * cannot fill the device sooner: the main kernel up to
  * a quarter of the device's resident lanes (one pair wave per SIMD; 32,768
  * signatures on 256 CUs), on eight lanes (two lane quads) up to one quad wave
- * per SIMD (8,192 signatures; STL_TUNE_QUAD), the point decoding on pairs up
- * to half of them.  Same accept bits; this flag turns both off (A/B and
+ * per SIMD (8,192 signatures) and on four (two duos) up to one duo wave per
+ * SIMD (16,384; STL_TUNE_QUAD), the point decoding on pairs up to half of
+ * them.  Same accept bits; this flag turns both off (A/B and
  * tests). */
 #define STL_ONE_LANE 0x10u
 /* TEST-ONLY: the raw crypto_sign_verify_detached predicate of the selected
