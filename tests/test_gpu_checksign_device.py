@@ -138,13 +138,15 @@ def test_signed_blob_verify_device_equals_two_step(stl, torch_cuda):
                 assert b1.sum() > 0.9 * n and (st != 0).sum() > 0  # mostly valid; some deferred / malformed
 
 
-def test_checksign_device_faults_are_errors(stl, torch_cuda, ledger):
+@pytest.mark.parametrize("m", [200_000, 1000])
+def test_checksign_device_faults_are_errors(stl, torch_cuda, ledger, m):
     """A failure injected at any HIP call of the one-call path returns a
-    negative code, never a reject bitmap, and the next clean call is exact."""
+    negative code, never a reject bitmap, and the next clean call is exact:
+    the two-stream chunked path (200,000 rows) and the small path whose point
+    role and key sample run beside the hashing (1,000 rows)."""
     from stellard_amd import _native as N
     torch = torch_cuda
     lp, d_pre, d_off, d_len, sig, pk = ledger
-    m = 200_000
     sl = slice(0, m)
     ref = stl.words_to_bool(stl.tx_verify_batch_device(d_pre, d_off[sl], d_len[sl], sig[sl], pk[sl]), m)
     torch.cuda.synchronize()
