@@ -1712,7 +1712,9 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     for (uint32_t j = 1; j < S; ++j)
       if ((e = hipStreamWaitEvent(x.streams[j], x.fork, 0)) != hipSuccess) return e;
   }
-  if (x.main_queue) {  // zero each stream's counters: one per chunk it runs
+  // zero each stream's counters, one per chunk it runs (a lone lane-pair or
+  // lane-group chunk uses none: one dependent memset less on the latency path)
+  if (x.main_queue && !(nchunks == 1 && pair_chunk(n, policy, x))) {
     for (uint32_t j = 0; j < S; ++j) {
       const uint64_t cj = (nchunks - j + S - 1) / S;
       e = hipMemsetAsync(queue_counters(x.ws[j], x.grid), 0, cj * 4, x.streams[j]);
