@@ -30,7 +30,11 @@ CSRC = os.path.join(ROOT, "stellard_amd", "csrc")
 
 
 def _deps(*extra):
-    d = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", "stl.h")]
+    # the host build compiles the __host__ __device__ headers only (hostemu.cpp
+    # includes no .hip / .cpp of the product), so kernel-launcher edits do not
+    # force the slow sanitizer rebuild
+    d = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
+        [os.path.join(ROOT, "include", "stl.h")]
     return d + [os.path.join(ROOT, "oracle", f) for f in ("stl_oracle.c", "stl_oracle_tx.c", "stl_oracle.h")] + \
         list(extra)
 
