@@ -161,7 +161,7 @@ const char *stl_strerror(int rc);
  * returned either way; a message longer than 2^32 - 1 bytes is STL_EINVAL
  * without a fallback and the fallback's answer (&& S < L) with one.
  * LATENCY: a signature's chain runs on eight GPU lanes (two lane quads), so a
- * call is latency-bound: 332 us per call on MI355X against libsodium's 31 us
+ * call is latency-bound: 295 us per call on MI355X against libsodium's 31 us
  * (round 4; 489 us on lane pairs in round 2), and concurrent calls
  * serialise on the device (tools/latency.py).
  * Callers that verify one signature at a time (stellard's JobQueue workers)

@@ -331,6 +331,8 @@ struct Device {
   std::map<hipStream_t, std::unique_ptr<StreamCtx>> stream_ws;  // workspace of every stream used
   std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;    // tx-hash work counter
   std::mutex ws_mu;
+  void* stage = nullptr;  // pinned host staging of small host batches (run_small), under mu
+  size_t stage_cap = 0;
   PhaseTimer timer;
   stl::PhaseClock clock{phase_mark, &timer};
 };
@@ -440,6 +442,9 @@ void release_device(Device& d) {
     b->release();
   for (auto& kv : d.stream_ws) kv.second->release();
   for (auto& kv : d.stream_ctr) kv.second->release();
+  if (d.stage) (void)hipHostFree(d.stage);
+  d.stage = nullptr;
+  d.stage_cap = 0;
   d.timer.release();
   for (hipStream_t s : {d.stream, d.stream2, d.stream3, d.copy})
     if (s) (void)hipStreamDestroy(s);
@@ -888,12 +893,61 @@ bool auto_dedup(uint32_t flags) {
   return (flags & (STL_DEDUP_KEYS | STL_NO_AUTO_DEDUP | STL_FULL_LENGTH)) == 0;
 }
 
+// Small signature batches on one device (single calls of
+// stl_ed25519_verify_detached, the request aggregator's batches): the rows
+// are staged in pinned host memory and sent by ONE copy on the kernel stream
+// -- no copy stream, no events, one synchronisation -- since at this size the
+// call is latency, not bandwidth.
+constexpr size_t kSmallBatch = 4096;
+
+int run_small(const Batch& b, size_t n) {
+  Device& d = *g_devs[0];
+  std::lock_guard<std::mutex> lk(d.mu);
+  STL_TRY(hipSetDevice(d.ordinal));
+  const size_t bytes = n * 128, words = (n + 63) / 64;
+  if (d.stage_cap < bytes + words * 8) {
+    if (d.stage) (void)hipHostFree(d.stage);
+    d.stage = nullptr;
+    d.stage_cap = 0;
+    const size_t cap = kSmallBatch * 128 + kSmallBatch / 8;
+    if (fault_now() || hipHostMalloc(&d.stage, cap, hipHostMallocDefault) != hipSuccess) {
+      d.stage = nullptr;
+      return STL_ENOMEM;
+    }
+    d.stage_cap = cap;
+  }
+  STL_RC(d.sig.ensure(bytes));
+  STL_RC(d.bitmap.ensure(words * 8));
+  uint8_t* st = static_cast<uint8_t*>(d.stage);
+  std::memcpy(st, b.sig, n * 64);
+  std::memcpy(st + 64 * n, b.msg32, n * 32);
+  std::memcpy(st + 96 * n, b.pk, n * 32);
+  uint8_t* dev = static_cast<uint8_t*>(d.sig.p);
+  auto go = [&]() -> int {
+    STL_TRY(hipMemcpyAsync(dev, st, bytes, hipMemcpyHostToDevice, d.stream));
+    STL_RC(run_verify(d, d.stream, dev, dev + 64 * n, dev + 96 * n, n, static_cast<uint64_t*>(d.bitmap.p),
+                      chunk_policy(b, 0, n), false, 1));
+    STL_TRY(hipMemcpyAsync(st + bytes, d.bitmap.p, words * 8, hipMemcpyDeviceToHost, d.stream));
+    STL_TRY(hipStreamSynchronize(d.stream));
+    return STL_OK;
+  };
+  const int rc = go();
+  if (rc) {  // nothing may still read the staging buffer
+    (void)hipStreamSynchronize(d.stream);
+    return rc;
+  }
+  std::memcpy(b.bitmap, st + bytes, (n + 7) / 8);
+  return STL_OK;
+}
+
 int run_batch(const Batch& b, size_t n, uint64_t* gather_ns) {
   if (n == 0) return STL_OK;
   STL_RC(ensure_init());
   DeviceGuard guard;  // the last shard and the gather run on this thread
   const int g = (int)g_devs.size();
   if (g == 0) return STL_ENODEV;
+  if (b.mode == Mode::kSig && n <= kSmallBatch && g == 1 && g_shards_per_device == 1 && !g_comm_gather)
+    return run_small(b, n);
   // one kernel launch handles up to 2^32-64 signatures per shard
   const size_t kMaxShard = (size_t)1 << 31;
   int gg = g * g_shards_per_device;
