@@ -72,20 +72,22 @@ extern "C" {
  * accept bits; costs a hash pass and extra device workspace: about 270 MB
  * (stl_kernels.h kDedupBytes: hash slots, key arrays, decoded keys, shared and
  * wide key tables), allocated once per device for the host batch API and once
- * per (device, stream) -- per library stream too -- for the device-resident
- * API; does not pay when keys are all distinct.  Chunks small enough for lane
+ * per (device, stream) -- per library stream too, and for at most
+ * STL_TUNE_STREAM_WORKSPACES caller streams -- for the device-resident API; does not pay when keys are all distinct.  Chunks small enough for lane
  * pairs or quads (STL_ONE_LANE below) run on them instead: latency-bound
  * there, the pairs and quads are faster. */
 #define STL_DEDUP_KEYS 0x8u
 /* The host batch calls (stl_ed25519_verify_batch, stl_tx_verify_batch, the
  * blob calls) choose STL_DEDUP_KEYS by themselves for every 64K-row chunk in
- * which a sample of 2,048 keys shows at least a quarter repeating (host-side,
- * about 20 us per chunk); this flag turns the automatic choice off (A/B and
- * callers that know their keys are distinct).  stl_ed25519_verify_batch_device
- * chooses by feedback instead (its keys are in HBM): each call ends with a
- * one-workgroup sample of its keys on the caller's stream, and the next call
- * on that stream follows that sample's verdict (no synchronisation; a stream's
- * first call runs without dedup).  The bits never depend on the choice. */
+ * which a host-side sample of 1,024 evenly spaced keys shows at least a fifth
+ * repeating an earlier one (about 40 us per chunk, overlapped with the earlier
+ * chunks' kernels); this flag turns the automatic choice off (A/B and callers
+ * that know their keys are distinct).  The device-resident verify and
+ * checkSign calls choose by feedback instead (their keys are in HBM): each
+ * call ends with a one-workgroup sample of 2,048 keys on the caller's stream
+ * (dedup when at least a quarter repeat), and the next call on that stream
+ * follows that sample's verdict (no synchronisation; a stream's first call
+ * runs without dedup).  The bits never depend on the choice. */
 #define STL_NO_AUTO_DEDUP 0x20u
 /* Small chunks run each signature on two lanes, which ends a launch that
  * cannot fill the device sooner: the main kernel up to
@@ -280,10 +282,25 @@ int stl_signed_blob_verify_batch_device(uint32_t kind, const uint8_t *d_blobs, c
  * stl_shard_range).  Setup: rank 0 calls stl_comm_unique_id and hands the
  * 128 bytes to every rank out of band (stellard: its own config; the bench:
  * torch.distributed over TCP); then every rank calls stl_comm_init_rank on its
- * initialised device (blocks until all ranks have joined). */
+ * initialised device, which blocks until all ranks have joined -- or until the
+ * RCCL deadline (STL_RCCL_TIMEOUT_S at stl_init, default 120 s, or
+ * STL_TUNE_RCCL_TIMEOUT_MS) passes: the communicator is then built
+ * nonblocking (ncclCommInitRankConfig, blocking = 0) and polled
+ * (ncclCommGetAsyncError); on the deadline it is aborted and the call returns
+ * STL_ERCCL, and a later stl_comm_init_rank may try again. */
 int stl_comm_unique_id(uint8_t id[128]);
 int stl_comm_init_rank(int nranks, int rank, const uint8_t id[128]);
 void stl_comm_destroy(void);
+/* Aborts the communicator (ncclCommAbort: outstanding collectives end without
+ * waiting for peers) -- the teardown after a failed or timed-out gather. */
+void stl_comm_abort(void);
+/* hipStreamSynchronize(stream) with the RCCL deadline (timeout_ms, or the
+ * library's when <= 0): while the stream has not drained, the communicator's
+ * asynchronous error is polled; an RCCL error or the deadline aborts the
+ * communicator (which ends a stalled gather's kernels) and returns
+ * STL_ERCCL, so a rank whose peers never arrive can fall back instead of
+ * hanging. */
+int stl_comm_sync(void *stream, int timeout_ms);
 /* What RCCL itself reports for the communicator libstl gathers over
  * (ncclCommCount / ncclCommUserRank): the one-process-per-GPU communicator of
  * stl_comm_init_rank if there is one, else the in-process communicator of
@@ -303,7 +320,11 @@ int stl_bitmap_gather_device(const uint64_t *d_words, size_t words_per_rank, uin
  * which land at word word_offsets[r] of d_all_words on rank root.
  * word_offsets: nranks+1 host entries, identical on every rank.  Grouped
  * ncclSend / ncclRecv (the root's own slice is a device copy); asynchronous
- * on stream.  STL_EINVAL if nwords disagrees with the offsets. */
+ * on stream.  STL_EINVAL if nwords disagrees with the offsets.  The argument
+ * checks are local to each rank and run before the group is posted: a rank
+ * that gets STL_EINVAL (its nwords, or a NULL d_all_words on the root) does
+ * not join, and its peers then block in their send / recv -- every rank must
+ * pass the same word_offsets and its own slice's size. */
 int stl_bitmap_gatherv_device(const uint64_t *d_words, size_t nwords, uint64_t *d_all_words,
                               const uint64_t *word_offsets, int root, void *stream);
 
@@ -413,7 +434,23 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
                                   quads (each group formula's four products one per lane), 2 = the
                                   next ones up to one wave per SIMD at four lanes on lane duos (two
                                   products per lane); 3 (default) both, 0 lane pairs only */
+#define STL_TUNE_STREAM_WORKSPACES 6 /* 1..64 (default 4, env STL_MAX_STREAM_WORKSPACES): caller streams
+                                        per device whose context (verify workspace ~0.44 GB, hash
+                                        queue, checkSign scratch) libstl keeps; the least recently
+                                        used one beyond it is freed */
+#define STL_TUNE_RCCL_TIMEOUT_MS 7 /* 1..3,600,000 (default 120,000; env STL_RCCL_TIMEOUT_S): deadline of
+                                      stl_comm_init_rank and stl_comm_sync */
 int stl_debug_tuning(int key, int value);
+/* Caller-stream contexts libstl currently keeps on the current device. */
+int stl_debug_stream_contexts(void);
+
+/* Frees libstl's context of a caller stream on the current device -- its
+ * verify workspace, hash queue, checkSign scratch and events -- after a device
+ * synchronisation (call it before destroying a stream the library has run
+ * on, or let the per-device cap, STL_TUNE_STREAM_WORKSPACES, evict it).  A
+ * call still running on that stream keeps the context until it returns.
+ * STL_EINVAL for one of libstl's own pool streams; STL_OK if there is none. */
+int stl_release_stream(void *stream);
 
 /* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;
  * EdKeyPair::setSeed, EdKeyPair.cpp:25-33): RFC 8032 keypair from a 32-byte

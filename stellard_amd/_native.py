@@ -42,6 +42,8 @@ STL_TUNE_STREAMS = 2
 STL_TUNE_CHUNK_LOG2 = 3
 STL_TUNE_BYTE_SHARDS = 4
 STL_TUNE_QUAD = 5
+STL_TUNE_STREAM_WORKSPACES = 6
+STL_TUNE_RCCL_TIMEOUT_MS = 7
 
 # per-transaction status of the serialized-transaction entry points
 STL_TX_OK = 0
@@ -86,6 +88,8 @@ SYMBOLS = [
     ("stl_comm_unique_id", ctypes.c_int, [_U8P]),
     ("stl_comm_init_rank", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _U8P]),
     ("stl_comm_destroy", None, []),
+    ("stl_comm_abort", None, []),
+    ("stl_comm_sync", ctypes.c_int, [_P, ctypes.c_int]),
     ("stl_comm_info", ctypes.c_int, [_P, _P]),
     ("stl_bitmap_gather_device", ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_int, _P]),
     ("stl_bitmap_gatherv_device", ctypes.c_int, [_P, ctypes.c_size_t, _P, _P, ctypes.c_int, _P]),
@@ -97,6 +101,8 @@ SYMBOLS = [
     ("stl_set_phase_timing", ctypes.c_int, [ctypes.c_int]),
     ("stl_debug_verify_k_device", ctypes.c_int, [_U8P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
     ("stl_debug_tuning", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("stl_debug_stream_contexts", ctypes.c_int, []),
+    ("stl_release_stream", ctypes.c_int, [_P]),
     ("stl_debug_sign_adversarial_device", ctypes.c_int,
      [_U8P, _U8P, _U8P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, _P]),
 ]

@@ -48,12 +48,31 @@ def _run(cmd, cwd=ROOT):
     subprocess.run(cmd, cwd=cwd, check=True)
 
 
+# per-object dependencies: the host sources see only the ABI header and the
+# launcher declarations, so a host-side change does not recompile the kernels
+# (about 100 s) -- the objects live in build/obj (git-ignored, never shipped)
+HOST_DEPS = ["stl_kernels.h", os.path.join("..", "..", "include", "stl.h")]
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+
+
 def build_product(force=False, extra_flags=()):
     out = os.path.join(ROOT, "stellard_amd", "libstl.so")
     deps = [os.path.join(CSRC, d) for d in PRODUCT_DEPS]
-    if force or extra_flags or _stale(out, deps):
+    if extra_flags:  # variant builds: one command, nothing cached
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *extra_flags,
               "-o", out] + [os.path.join(CSRC, s) for s in PRODUCT_SRCS])
+        return out
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    objs = []
+    for src in PRODUCT_SRCS:
+        obj = os.path.join(OBJ_DIR, src + ".o")
+        sdeps = deps if src.endswith(".hip") else [os.path.join(CSRC, d) for d in [src] + HOST_DEPS]
+        if force or _stale(obj, sdeps):
+            _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-o", obj,
+                  os.path.join(CSRC, src)])
+        objs.append(obj)
+    if force or _stale(out, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", out] + objs)
     return out
 
 

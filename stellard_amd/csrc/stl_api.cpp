@@ -90,6 +90,11 @@ struct Rccl {
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
   decltype(&ncclCommCount) CommCount = nullptr;
   decltype(&ncclCommUserRank) CommUserRank = nullptr;
+  // nonblocking bring-up with a deadline; optional symbols
+  decltype(&ncclCommInitRankConfig) CommInitRankConfig = nullptr;
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+  decltype(&ncclCommAbort) CommAbort = nullptr;
+  bool nonblocking() const { return CommInitRankConfig && CommGetAsyncError && CommAbort; }
 
   template <typename F>
   static bool sym(void* h, const char* name, F& f) {
@@ -107,11 +112,34 @@ struct Rccl {
            sym(h, "ncclGather", Gather) && sym(h, "ncclAllGather", AllGather) && sym(h, "ncclSend", Send) &&
            sym(h, "ncclRecv", Recv) && sym(h, "ncclGroupStart", GroupStart) && sym(h, "ncclGroupEnd", GroupEnd) &&
            sym(h, "ncclCommCount", CommCount) && sym(h, "ncclCommUserRank", CommUserRank);
+      (void)(sym(h, "ncclCommInitRankConfig", CommInitRankConfig) &&
+             sym(h, "ncclCommGetAsyncError", CommGetAsyncError) && sym(h, "ncclCommAbort", CommAbort));
     });
     return ok;
   }
 };
 Rccl g_rccl;
+
+// Deadline of the one-process-per-GPU communicator's RCCL operations: the
+// bring-up (a rank that never joins would block ncclCommInitRank forever) and
+// stl_comm_sync's wait on a gather.  STL_RCCL_TIMEOUT_S at stl_init, or
+// STL_TUNE_RCCL_TIMEOUT_MS.
+std::atomic<int> g_rccl_timeout_ms{120000};
+
+// Settles a nonblocking communicator's call that returned r: ncclInProgress
+// is polled (ncclCommGetAsyncError) until it completes or the deadline
+// passes.  STL_OK, or STL_ERCCL on an error or a timeout (the caller aborts).
+int rccl_settle(ncclComm_t comm, ncclResult_t r) {
+  if (r == ncclSuccess) return STL_OK;
+  if (r != ncclInProgress || !comm || !g_rccl.CommGetAsyncError) return STL_ERCCL;
+  const auto end = std::chrono::steady_clock::now() + std::chrono::milliseconds(g_rccl_timeout_ms.load());
+  ncclResult_t st = ncclInProgress;
+  while (g_rccl.CommGetAsyncError(comm, &st) == ncclSuccess && st == ncclInProgress) {
+    if (std::chrono::steady_clock::now() > end) return STL_ERCCL;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  return st == ncclSuccess ? STL_OK : STL_ERCCL;
+}
 
 struct DevBuf {
   void* p = nullptr;
@@ -276,10 +304,22 @@ uint32_t chunk_for(uint32_t grid, size_t n) {
 // stream uses that stream's workspace, in stream order -- the caller's streams
 // (device-resident API) and the library's own pool streams alike, so a pool
 // stream shared by several callers and both APIs needs only one.  `mu` is
-// held while a launch is planned and enqueued (the workspace may grow).
+// held while a launch is planned and enqueued (the workspace may grow), and
+// every buffer below is only grown or read under it (the hash
+// queue of a shared pool stream was grown outside it).  Caller streams'
+// contexts are capped per device (kMaxCallerStreams, least recently used
+// evicted) and stl_release_stream drops one: a context lives on in a
+// shared_ptr until its last user returns, and frees its device memory after a
+// device synchronisation (its stream may be gone by then).
 struct StreamCtx {
   std::mutex mu;
+  int ordinal = -1;        // device of the buffers below
+  bool pool = false;       // a library pool stream's context (never evicted)
+  uint64_t last_use = 0;   // LRU tick (Device::ws_mu)
   DevBuf ws;
+  // work counter + longest-first order of the device-resident hash kernels
+  // (stl::hash_queue_bytes(n)) of the launches on this stream
+  DevBuf queue;
   // fork / join events of launches whose chunks this (caller) stream spreads
   // over pool streams
   hipEvent_t fork = nullptr;
@@ -298,12 +338,25 @@ struct StreamCtx {
     auto_flag = auto_flag_dev = nullptr;
     scratch.release();
     ws.release();
+    queue.release();
     for (hipEvent_t& e : join) {
       if (e) (void)hipEventDestroy(e);
       e = nullptr;
     }
     if (fork) (void)hipEventDestroy(fork);
     fork = nullptr;
+  }
+  bool holds_memory() const { return auto_flag || scratch.p || ws.p || queue.p || fork; }
+  ~StreamCtx() {
+    if (!holds_memory() || ordinal < 0) return;
+    // an evicted or released context: its kernels (and the key sample's
+    // write to auto_flag) may still be in flight on a stream that the caller
+    // may have destroyed since, so wait for the whole device
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(ordinal) == hipSuccess) (void)hipDeviceSynchronize();
+    release();
+    if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
 
@@ -323,13 +376,17 @@ struct Device {
   hipStream_t stream = nullptr;   // kernel stream 0: host batch API even chunks and results
   hipStream_t stream2 = nullptr;  // kernel stream 1: host API odd chunks; a device call's second stream
   hipStream_t copy = nullptr;     // host-to-device copies (overlap the previous chunk's kernels)
-  hipStream_t stream3 = nullptr;  // a device call's fourth stream (STL_TUNE_STREAMS 4 only; made on use)
+  // a device call's fourth stream (STL_TUNE_STREAMS 4 only; made on use under
+  // ws_mu, read without a lock by drain / run_verify -- ADVICE r4)
+  std::atomic<hipStream_t> stream3{nullptr};
   ncclComm_t comm = nullptr;      // in-process communicator (rank = device index)
   std::mutex mu;
   DevBuf sig, msg, pk, bitmap, pre, off, len, ctr, ctr2, txid, status, wide, gather;
   DevBuf counters;  // device u64 counters of stl_get_stats: [0] accepted, [1] full-length lanes
-  std::map<hipStream_t, std::unique_ptr<StreamCtx>> stream_ws;  // workspace of every stream used
-  std::map<hipStream_t, std::unique_ptr<DevBuf>> stream_ctr;    // tx-hash work counter
+  // workspace of every stream used: the pool streams' for good, at most
+  // kMaxCallerStreams caller streams' (LRU)
+  std::map<hipStream_t, std::shared_ptr<StreamCtx>> stream_ws;
+  uint64_t ws_tick = 0;
   std::mutex ws_mu;
   void* stage = nullptr;  // pinned host staging of small host batches (run_small), under mu
   size_t stage_cap = 0;
@@ -433,22 +490,31 @@ int setup_device(Device& d) {
 
 void release_device(Device& d) {
   (void)hipSetDevice(d.ordinal);
-  for (hipStream_t s : {d.stream, d.stream2, d.stream3, d.copy})
+  const hipStream_t s3 = d.stream3.load();
+  for (hipStream_t s : {d.stream, d.stream2, s3, d.copy})
     if (s) (void)hipStreamSynchronize(s);
+  (void)hipDeviceSynchronize();  // caller streams' work on the workspaces freed below
   if (d.comm && g_rccl.ok) (void)g_rccl.CommDestroy(d.comm);
   d.comm = nullptr;
   for (DevBuf* b : {&d.sig, &d.msg, &d.pk, &d.bitmap, &d.pre, &d.off, &d.len, &d.ctr, &d.ctr2, &d.txid, &d.status,
                     &d.wide, &d.gather, &d.counters})
     b->release();
-  for (auto& kv : d.stream_ws) kv.second->release();
-  for (auto& kv : d.stream_ctr) kv.second->release();
+  {
+    std::lock_guard<std::mutex> lk(d.ws_mu);
+    for (auto& kv : d.stream_ws) {
+      std::lock_guard<std::mutex> cl(kv.second->mu);
+      kv.second->release();
+    }
+    d.stream_ws.clear();
+  }
   if (d.stage) (void)hipHostFree(d.stage);
   d.stage = nullptr;
   d.stage_cap = 0;
   d.timer.release();
-  for (hipStream_t s : {d.stream, d.stream2, d.stream3, d.copy})
+  for (hipStream_t s : {d.stream, d.stream2, s3, d.copy})
     if (s) (void)hipStreamDestroy(s);
-  d.stream = d.stream2 = d.stream3 = d.copy = nullptr;
+  d.stream = d.stream2 = d.copy = nullptr;
+  d.stream3.store(nullptr);
 }
 
 int ensure_init() {
@@ -459,12 +525,57 @@ int ensure_init() {
   return stl_init(nullptr);
 }
 
-// The verify workspace of stream s on device d (created on first use).
-StreamCtx& stream_ctx(Device& d, hipStream_t s) {
+// Caller streams whose contexts a device keeps: each holds a
+// verify workspace (stl::verify_ws_bytes: ~0.44 GB, ~0.7 GB with key dedup),
+// so a caller cycling through many streams must not grow device memory
+// without bound.  STL_MAX_STREAM_WORKSPACES overrides (1..64) at stl_init.
+constexpr int kDefaultCallerStreams = 4;
+std::atomic<int> g_max_caller_streams{kDefaultCallerStreams};
+
+bool is_pool_stream(const Device& d, hipStream_t s) {
+  return s && (s == d.stream || s == d.stream2 || s == d.copy || s == d.stream3.load());
+}
+
+// The context of stream s on device d (created on first use).  Creating a
+// caller stream's context beyond the cap evicts the least recently used
+// caller context; the evicted one is destroyed (device sync + free) outside
+// ws_mu, once its last user has let go.
+std::shared_ptr<StreamCtx> stream_ctx(Device& d, hipStream_t s) {
+  std::shared_ptr<StreamCtx> evicted;
+  std::shared_ptr<StreamCtx> out;
+  {
+    std::lock_guard<std::mutex> lk(d.ws_mu);
+    auto& slot = d.stream_ws[s];
+    if (!slot) {
+      slot = std::make_shared<StreamCtx>();
+      slot->ordinal = d.ordinal;
+      slot->pool = is_pool_stream(d, s);
+      if (!slot->pool) {
+        int callers = 0;
+        auto lru = d.stream_ws.end();
+        for (auto it = d.stream_ws.begin(); it != d.stream_ws.end(); ++it) {
+          if (it->second->pool) continue;
+          ++callers;
+          if (it->first != s && (lru == d.stream_ws.end() || it->second->last_use < lru->second->last_use)) lru = it;
+        }
+        if (callers > g_max_caller_streams.load() && lru != d.stream_ws.end()) {
+          evicted = std::move(lru->second);
+          d.stream_ws.erase(lru);
+        }
+      }
+    }
+    d.stream_ws[s]->last_use = ++d.ws_tick;
+    out = d.stream_ws[s];
+  }
+  return out;  // `evicted` (if any) is destroyed here, without ws_mu
+}
+
+// Caller contexts currently kept on device d (tests: the cap holds).
+int caller_contexts(Device& d) {
   std::lock_guard<std::mutex> lk(d.ws_mu);
-  auto& slot = d.stream_ws[s];
-  if (!slot) slot.reset(new StreamCtx());
-  return *slot;
+  int k = 0;
+  for (auto& kv : d.stream_ws) k += kv.second->pool ? 0 : 1;
+  return k;
 }
 
 // Per-lane workspace slots (workgroups) for launch_verify: room for two lanes
@@ -516,17 +627,25 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   hipStream_t pool[stl::kMaxVerifyStreams] = {s};
   uint32_t np = 1;
   if (S > 1) {
-    if (S > 3 && !d.stream3) {
+    if (S > 3 && !d.stream3.load()) {
       std::lock_guard<std::mutex> lk(d.ws_mu);
-      if (!d.stream3) STL_TRY(hipStreamCreateWithFlags(&d.stream3, hipStreamNonBlocking));
+      if (!d.stream3.load()) {
+        hipStream_t s3 = nullptr;
+        STL_TRY(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+        d.stream3.store(s3);
+      }
     }
-    for (hipStream_t p : {d.stream2, d.stream, d.stream3})
+    for (hipStream_t p : {d.stream2, d.stream, d.stream3.load()})
       if (np < S && p && p != s) pool[np++] = p;
   }
   S = np;
   x.nstreams = S;
+  std::shared_ptr<StreamCtx> hold[stl::kMaxVerifyStreams];
   StreamCtx* ctx[stl::kMaxVerifyStreams];
-  for (uint32_t j = 0; j < S; ++j) ctx[j] = &stream_ctx(d, pool[j]);
+  for (uint32_t j = 0; j < S; ++j) {
+    hold[j] = stream_ctx(d, pool[j]);
+    ctx[j] = hold[j].get();
+  }
   StreamCtx* order[stl::kMaxVerifyStreams];
   std::copy(ctx, ctx + S, order);
   std::sort(order, order + S);
@@ -551,14 +670,12 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   return STL_OK;
 }
 
-// Work-queue workspace for (device, stream) of the device-resident hash
-// kernels (counter + longest-first order, stl::hash_queue_bytes(n)).
-int stream_queue(Device& d, hipStream_t s, size_t n, uint32_t** qws) {
-  std::lock_guard<std::mutex> lk(d.ws_mu);
-  auto& slot = d.stream_ctr[s];
-  if (!slot) slot.reset(new DevBuf());
-  STL_RC(slot->ensure(stl::hash_queue_bytes(n)));
-  *qws = static_cast<uint32_t*>(slot->p);
+// Hash work queue of stream context c for n rows (counter + longest-first
+// order, stl::hash_queue_bytes(n)).  Caller holds c.mu until the hash kernel
+// using it is enqueued (a concurrent grow would free it first -- ADVICE r4).
+int ctx_queue(StreamCtx& c, size_t n, uint32_t** qws) {
+  STL_RC(c.queue.ensure(stl::hash_queue_bytes(n)));
+  *qws = static_cast<uint32_t*>(c.queue.p);
   return STL_OK;
 }
 
@@ -769,9 +886,9 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
   // chunk, so no workspace grows while earlier chunks still run on it
   if (b.auto_dedup && n > kPipeChunk / 2)
     for (hipStream_t ks : {d.stream, d.stream2}) {
-      StreamCtx& c = stream_ctx(d, ks);
-      std::lock_guard<std::mutex> lk(c.mu);
-      STL_RC(c.ws.ensure(stl::verify_ws_bytes(d.grid, true)));
+      const std::shared_ptr<StreamCtx> c = stream_ctx(d, ks);
+      std::lock_guard<std::mutex> lk(c->mu);
+      STL_RC(c->ws.ensure(stl::verify_ws_bytes(d.grid, true)));
     }
   if (two && b.mode != Mode::kSig) STL_RC(d.ctr2.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
   for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
@@ -811,7 +928,8 @@ int drain(Device& d) {
   const hipError_t a = hipStreamSynchronize(d.copy);
   const hipError_t b = hipStreamSynchronize(d.stream);
   const hipError_t c = hipStreamSynchronize(d.stream2);
-  const hipError_t e = d.stream3 ? hipStreamSynchronize(d.stream3) : hipSuccess;
+  const hipStream_t s3 = d.stream3.load();
+  const hipError_t e = s3 ? hipStreamSynchronize(s3) : hipSuccess;
   return (a == hipSuccess && b == hipSuccess && c == hipSuccess && e == hipSuccess) ? STL_OK : STL_EHIP;
 }
 
@@ -1021,6 +1139,10 @@ int stl_init(const stl_config* cfg) {
     // profiling runs use STL_STREAMS=1 so that kernels do not overlap)
     const int s = env_int("STL_STREAMS", 0), c = env_int("STL_CHUNK_LOG2", 0);
     if (s >= 1 && s <= (int)stl::kMaxVerifyStreams) g_tune_streams.store(s);
+    const int to = env_int("STL_RCCL_TIMEOUT_S", 0);
+    if (to > 0 && to <= 3600) g_rccl_timeout_ms.store(to * 1000);
+    const int ws = env_int("STL_MAX_STREAM_WORKSPACES", 0);
+    if (ws >= 1 && ws <= 64) g_max_caller_streams.store(ws);
     if (c >= 15 && c <= 20) g_tune_sub_log2.store(c);
   }
   int first = 0, want = -1, spd = 1;
@@ -1144,6 +1266,8 @@ int stl_debug_tuning(int key, int value) {
       case STL_TUNE_CHUNK_LOG2: return g_tune_sub_log2.load();
       case STL_TUNE_BYTE_SHARDS: return g_tune_byte_shards.load();
       case STL_TUNE_QUAD: return g_tune_quad.load();
+      case STL_TUNE_STREAM_WORKSPACES: return g_max_caller_streams.load();
+      case STL_TUNE_RCCL_TIMEOUT_MS: return g_rccl_timeout_ms.load();
       default: return STL_EINVAL;
     }
   }
@@ -1166,9 +1290,41 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_QUAD:
       if (value < 0 || value > 3) return STL_EINVAL;
       return g_tune_quad.exchange(value);
+    case STL_TUNE_STREAM_WORKSPACES:  // applies as caller contexts are next created
+      if (value < 1 || value > 64) return STL_EINVAL;
+      return g_max_caller_streams.exchange(value);
+    case STL_TUNE_RCCL_TIMEOUT_MS:
+      if (value < 1 || value > 3600000) return STL_EINVAL;
+      return g_rccl_timeout_ms.exchange(value);
     default:
       return STL_EINVAL;
   }
+}
+
+int stl_release_stream(void* stream) {
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  std::shared_ptr<StreamCtx> gone;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_init) return STL_OK;
+    const int di = current_device_index();
+    if (di < 0) return STL_ENODEV;
+    Device& d = *g_devs[di];
+    if (is_pool_stream(d, s)) return STL_EINVAL;
+    std::lock_guard<std::mutex> wl(d.ws_mu);
+    auto it = d.stream_ws.find(s);
+    if (it == d.stream_ws.end()) return STL_OK;
+    gone = std::move(it->second);
+    d.stream_ws.erase(it);
+  }
+  return STL_OK;  // `gone` synchronises the device and frees here, once no call holds it
+}
+
+int stl_debug_stream_contexts(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_init) return 0;
+  const int di = current_device_index();
+  return di < 0 ? STL_ENODEV : caller_contexts(*g_devs[di]);
 }
 
 int stl_get_stats(stl_stats* out) {
@@ -1379,10 +1535,11 @@ namespace {
 // call on that stream uses -- no synchronisation, a few microseconds of GPU
 // time.  A stream's first call, or a call issued before the previous call's
 // sample has run, uses the last verdict seen (initially: no dedup).
-int auto_dedup_device(Device& d, hipStream_t s, uint32_t flags, uint32_t* mode, uint32_t** flag_dev) {
+// c: the caller stream's context, kept alive by the caller until the sample
+// kernel writing *flag_dev is enqueued.
+int auto_dedup_device(StreamCtx& c, uint32_t flags, uint32_t* mode, uint32_t** flag_dev) {
   *flag_dev = nullptr;
   if (!auto_dedup(flags)) return STL_OK;
-  StreamCtx& c = stream_ctx(d, s);
   std::lock_guard<std::mutex> lk(c.mu);
   if (!c.auto_flag) {
     void* p = nullptr;
@@ -1420,10 +1577,6 @@ namespace {
 int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const uint8_t* bytes, const uint64_t* off,
                      const uint32_t* len, const uint8_t* sig_in, const uint8_t* pk_in, size_t n, uint64_t* words,
                      uint8_t* status, uint8_t* id, uint32_t flags) {
-  uint32_t mode = stl::kernel_mode(flags);
-  uint32_t* flag_dev = nullptr;
-  STL_RC(auto_dedup_device(d, s, flags, &mode, &flag_dev));
-  const bool dedup = (mode & stl::kModeDedupKeys) != 0;
   const stl::PhaseClock* clock = phase_clock(d);
   // chunks and streams as a device-resident verify call
   size_t sub = chunk_for(d.grid, n);
@@ -1433,8 +1586,14 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     sub = std::min<size_t>(n, stl::kPreChunk);
   }
   hipStream_t ks[2] = {s, s == d.stream2 ? d.stream : d.stream2};
-  StreamCtx* kc[2] = {&stream_ctx(d, ks[0]), S > 1 ? &stream_ctx(d, ks[1]) : nullptr};
+  const std::shared_ptr<StreamCtx> hold[2] = {stream_ctx(d, ks[0]),
+                                              S > 1 ? stream_ctx(d, ks[1]) : std::shared_ptr<StreamCtx>()};
+  StreamCtx* kc[2] = {hold[0].get(), hold[1].get()};
   StreamCtx& c = *kc[0];
+  uint32_t mode = stl::kernel_mode(flags);
+  uint32_t* flag_dev = nullptr;
+  STL_RC(auto_dedup_device(c, flags, &mode, &flag_dev));
+  const bool dedup = (mode & stl::kModeDedupKeys) != 0;
   // One chunk whose phase 1 runs as the two-role lane-pair kernel (small
   // batches; not blobs, whose signatures and keys come out of the pass): its
   // point role -- the two square-root chains, which need no message -- and
@@ -1458,13 +1617,15 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   };
   const bool ahead = S == 1 && !blob && !clock && n <= stl::kPreChunk &&
                      stl::verify_pair_points((uint32_t)n, mode, exec_for((uint32_t)n, 0));
-  uint32_t* q[2] = {nullptr, nullptr};
-  STL_RC(stream_queue(d, ks[0], S > 1 ? sub : n, &q[0]));
-  if (S > 1) STL_RC(stream_queue(d, ks[1], n - sub, &q[1]));
   std::vector<std::unique_lock<std::mutex>> locks;
   if (S > 1 && kc[1] < kc[0]) locks.emplace_back(kc[1]->mu);
   locks.emplace_back(c.mu);
   if (S > 1 && kc[1] > kc[0]) locks.emplace_back(kc[1]->mu);
+  // the hash queues under the locks held through the launches below: pool
+  // stream 1's context is shared by every caller stream
+  uint32_t* q[2] = {nullptr, nullptr};
+  STL_RC(ctx_queue(*kc[0], S > 1 ? sub : n, &q[0]));
+  if (S > 1) STL_RC(ctx_queue(*kc[1], n - sub, &q[1]));
   const size_t row = blob ? 128 : 32;
   STL_RC(c.scratch.ensure(std::max<size_t>(n, 1) * row));
   uint8_t* msg = static_cast<uint8_t*>(c.scratch.p);
@@ -1572,9 +1733,10 @@ int stl_ed25519_verify_batch_device(const uint8_t* d_sig, const uint8_t* d_msg, 
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const std::shared_ptr<StreamCtx> c = stream_ctx(*d, s);  // alive until the sample kernel is enqueued
   uint32_t mode = stl::kernel_mode(flags);
   uint32_t* flag_dev = nullptr;
-  STL_RC(auto_dedup_device(*d, s, flags, &mode, &flag_dev));
+  STL_RC(auto_dedup_device(*c, flags, &mode, &flag_dev));
   STL_RC(run_verify(*d, s, d_sig, d_msg, d_pk, n, d_bitmap_words, mode, false, g_tune_streams.load()));
   if (flag_dev) STL_TRY(stl::launch_key_sample(d_pk, (uint32_t)n, flag_dev, s));
   return STL_OK;
@@ -1600,8 +1762,10 @@ int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offse
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const std::shared_ptr<StreamCtx> c = stream_ctx(*d, s);
+  std::lock_guard<std::mutex> lk(c->mu);
   uint32_t* ctr = nullptr;
-  STL_RC(stream_queue(*d, s, n, &ctr));
+  STL_RC(ctx_queue(*c, n, &ctr));
   STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(*d), s));
   return STL_OK;
 }
@@ -1616,8 +1780,10 @@ int stl_signed_blob_prepare_device(uint32_t kind, const uint8_t* d_blobs, const 
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const std::shared_ptr<StreamCtx> c = stream_ctx(*d, s);
+  std::lock_guard<std::mutex> lk(c->mu);
   uint32_t* ctr = nullptr;
-  STL_RC(stream_queue(*d, s, n, &ctr));
+  STL_RC(ctx_queue(*c, n, &ctr));
   STL_TRY(stl::launch_tx_blob(d_blobs, d_offset, d_len, (uint32_t)n, d_msg, d_sig, d_pk, d_id, d_status, ctr,
                               hash_grid(*d), s, kind));
   return STL_OK;
@@ -1637,10 +1803,10 @@ int stl_ed25519_sign_batch_device(const uint8_t* d_seed, const uint8_t* d_msg, s
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  StreamCtx& c = stream_ctx(*d, s);
-  std::lock_guard<std::mutex> lk(c.mu);
-  STL_RC(c.ws.ensure(stl::verify_ws_bytes(d->grid)));
-  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws.p), grid_for(*d, n), s));
+  const std::shared_ptr<StreamCtx> c = stream_ctx(*d, s);
+  std::lock_guard<std::mutex> lk(c->mu);
+  STL_RC(c->ws.ensure(stl::verify_ws_bytes(d->grid)));
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c->ws.p), grid_for(*d, n), s));
   return STL_OK;
 }
 
@@ -1653,10 +1819,10 @@ int stl_debug_sign_adversarial_device(const uint8_t* d_seed, const uint8_t* d_ms
   Device* d = nullptr;
   STL_RC(device_for_call(&d));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  StreamCtx& c = stream_ctx(*d, s);
-  std::lock_guard<std::mutex> lk(c.mu);
-  STL_RC(c.ws.ensure(stl::verify_ws_bytes(d->grid)));
-  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c.ws.p), grid_for(*d, n), s,
+  const std::shared_ptr<StreamCtx> c = stream_ctx(*d, s);
+  std::lock_guard<std::mutex> lk(c->mu);
+  STL_RC(c->ws.ensure(stl::verify_ws_bytes(d->grid)));
+  STL_TRY(stl::launch_sign(d_seed, d_msg, (uint32_t)n, d_pk, d_sig, static_cast<uint4*>(c->ws.p), grid_for(*d, n), s,
                            d_cls, d_param, d_msg_out));
   return STL_OK;
 }
@@ -1683,7 +1849,21 @@ int stl_comm_init_rank(int nranks, int rank, const uint8_t id[128]) {
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
   ncclComm_t c = nullptr;
-  STL_RCCL_TRY(g_rccl.CommInitRank(&c, nranks, u, rank));
+  if (g_rccl.nonblocking()) {
+    // nonblocking bring-up polled against the deadline: a rank that never
+    // joins costs STL_ERCCL after STL_RCCL_TIMEOUT_S, not a hung process
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    if (fault_now()) return STL_ERCCL;
+    const ncclResult_t r = g_rccl.CommInitRankConfig(&c, nranks, u, rank, &cfg);
+    const int rc = c ? rccl_settle(c, r) : STL_ERCCL;
+    if (rc) {
+      if (c) (void)g_rccl.CommAbort(c);
+      return rc;
+    }
+  } else {
+    STL_RCCL_TRY(g_rccl.CommInitRank(&c, nranks, u, rank));
+  }
   g_pcomm = c;
   g_pcomm_ranks = nranks;
   return STL_OK;
@@ -1694,6 +1874,40 @@ void stl_comm_destroy(void) {
   if (g_pcomm && g_rccl.ok) (void)g_rccl.CommDestroy(g_pcomm);
   g_pcomm = nullptr;
   g_pcomm_ranks = 0;
+}
+
+void stl_comm_abort(void) {
+  std::lock_guard<std::mutex> lk(g_pcomm_mu);
+  if (g_pcomm && g_rccl.ok) (void)(g_rccl.CommAbort ? g_rccl.CommAbort(g_pcomm) : g_rccl.CommDestroy(g_pcomm));
+  g_pcomm = nullptr;
+  g_pcomm_ranks = 0;
+}
+
+int stl_comm_sync(void* stream, int timeout_ms) {
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const int ms = timeout_ms > 0 ? timeout_ms : g_rccl_timeout_ms.load();
+  const auto end = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return STL_OK;
+    if (q != hipErrorNotReady) return STL_EHIP;
+    {
+      std::lock_guard<std::mutex> lk(g_pcomm_mu);
+      ncclResult_t st = ncclSuccess;
+      const bool failed = g_pcomm && g_rccl.CommGetAsyncError &&
+                          (g_rccl.CommGetAsyncError(g_pcomm, &st) != ncclSuccess ||
+                           (st != ncclSuccess && st != ncclInProgress));
+      if (failed || std::chrono::steady_clock::now() > end) {
+        // a stalled or failed collective: abort the communicator, which ends
+        // its kernels, so the stream drains and the caller can fall back
+        if (g_pcomm && g_rccl.ok) (void)(g_rccl.CommAbort ? g_rccl.CommAbort(g_pcomm) : ncclSuccess);
+        g_pcomm = nullptr;
+        g_pcomm_ranks = 0;
+        return STL_ERCCL;
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
 }
 
 int stl_comm_info(int* nranks, int* rank) {
@@ -1721,13 +1935,15 @@ int stl_bitmap_gather_device(const uint64_t* d_words, size_t words_per_rank, uin
   if (!g_pcomm) return STL_ERCCL;
   if (!d_words || words_per_rank == 0 || root >= g_pcomm_ranks) return STL_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (fault_now()) return STL_ERCCL;
+  ncclResult_t r;
   if (root < 0) {
     if (!d_all_words) return STL_EINVAL;
-    STL_RCCL_TRY(g_rccl.AllGather(d_words, d_all_words, words_per_rank, ncclUint64, g_pcomm, s));
+    r = g_rccl.AllGather(d_words, d_all_words, words_per_rank, ncclUint64, g_pcomm, s);
   } else {
-    STL_RCCL_TRY(g_rccl.Gather(d_words, d_all_words, words_per_rank, ncclUint64, root, g_pcomm, s));
+    r = g_rccl.Gather(d_words, d_all_words, words_per_rank, ncclUint64, root, g_pcomm, s);
   }
-  return STL_OK;
+  return rccl_settle(g_pcomm, r);  // a nonblocking communicator may answer ncclInProgress
 }
 
 int stl_bitmap_gatherv_device(const uint64_t* d_words, size_t nwords, uint64_t* d_all_words,
@@ -1758,8 +1974,8 @@ int stl_bitmap_gatherv_device(const uint64_t* d_words, size_t nwords, uint64_t* 
       if (g_rccl.Recv(d_all_words + word_offsets[r], w, ncclUint64, r, g_pcomm, s) != ncclSuccess) rc = STL_ERCCL;
     }
   }
-  if (g_rccl.GroupEnd() != ncclSuccess && rc == STL_OK) rc = STL_ERCCL;
-  return rc;
+  const int erc = rccl_settle(g_pcomm, g_rccl.GroupEnd());
+  return rc ? rc : erc;
 }
 
 }  // extern "C"

@@ -343,17 +343,22 @@ def tx_verify_batch_device(preimages, offsets, lengths, sig, pk, out_words=None,
 
 
 def signed_blob_verify_batch_device(blobs, offsets, lengths, out_words=None, tx_ids=False,
-                                    policy=POLICY_SODIUM_1_0_18, stream=None, kind=None):
+                                    policy=POLICY_SODIUM_1_0_18, stream=None, kind=None, out_status=None,
+                                    out_ids=None):
     """stl_signed_blob_verify_batch_device: checkSign from serialized objects
-    in HBM in one call -> dict of words (bitmap), status and (tx_ids) tx_id."""
+    in HBM in one call -> dict of words (bitmap), status and (tx_ids or
+    out_ids) tx_id."""
     import torch
     n = offsets.shape[0]
     dev = blobs.device
     if out_words is None:
         out_words = torch.empty(((n + 63) // 64,), dtype=torch.int64, device=dev)
-    status = torch.empty((n,), dtype=torch.uint8, device=dev)
-    tx_id = torch.empty((n, 32), dtype=torch.uint8, device=dev) if tx_ids else None
-    _check_rows(blobs, offsets, lengths, out_words)
+    status = torch.empty((n,), dtype=torch.uint8, device=dev) if out_status is None else out_status
+    tx_id = out_ids if out_ids is not None else (torch.empty((n, 32), dtype=torch.uint8, device=dev)
+                                                 if tx_ids else None)
+    if status.numel() < n or (tx_id is not None and tx_id.numel() < 32 * n):
+        raise ValueError("status / id buffers smaller than the batch")
+    _check_rows(blobs, offsets, lengths, out_words, status, tx_id)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     N.check(N.load().stl_signed_blob_verify_batch_device(
         N.STL_BLOB_TRANSACTION if kind is None else kind, p(blobs), p(offsets), p(lengths), n, p(out_words),
@@ -485,6 +490,17 @@ def comm_destroy():
     N.load().stl_comm_destroy()
 
 
+def comm_abort():
+    """stl_comm_abort: tear the communicator down without waiting for peers."""
+    N.load().stl_comm_abort()
+
+
+def comm_sync(stream=None, timeout_ms=0):
+    """stl_comm_sync: wait for ``stream`` under the RCCL deadline; raises
+    StlError (STL_ERCCL) after aborting the communicator if a gather stalls."""
+    N.check(N.load().stl_comm_sync(_stream_ptr(stream), int(timeout_ms)), "stl_comm_sync")
+
+
 def comm_info():
     """stl_comm_info: (nranks, rank) as RCCL reports them (ncclCommCount /
     ncclCommUserRank) for the communicator libstl gathers over."""
@@ -578,6 +594,8 @@ TUNE_FUSED_PREP, TUNE_MAIN_QUEUE = N.STL_TUNE_FUSED_PREP, N.STL_TUNE_MAIN_QUEUE
 TUNE_STREAMS, TUNE_CHUNK_LOG2 = N.STL_TUNE_STREAMS, N.STL_TUNE_CHUNK_LOG2
 TUNE_BYTE_SHARDS = N.STL_TUNE_BYTE_SHARDS
 TUNE_QUAD = N.STL_TUNE_QUAD
+TUNE_STREAM_WORKSPACES = N.STL_TUNE_STREAM_WORKSPACES
+TUNE_RCCL_TIMEOUT_MS = N.STL_TUNE_RCCL_TIMEOUT_MS
 
 
 def debug_tuning(key, value):
@@ -586,6 +604,21 @@ def debug_tuning(key, value):
     rc = N.load().stl_debug_tuning(key, value)
     if rc < 0:
         raise N.StlError(rc, "stl_debug_tuning")
+    return rc
+
+
+def release_stream(stream):
+    """stl_release_stream: free libstl's context of a caller stream (a torch
+    stream) on the current device."""
+    N.check(N.load().stl_release_stream(_stream_ptr(stream)), "stl_release_stream")
+
+
+def stream_contexts():
+    """Caller-stream contexts libstl keeps on the current device
+    (at most debug_tuning(TUNE_STREAM_WORKSPACES, -1))."""
+    rc = N.load().stl_debug_stream_contexts()
+    if rc < 0:
+        N.check(rc, "stl_debug_stream_contexts")
     return rc
 
 

@@ -358,3 +358,193 @@ def ledger_mutations(lp):
 
 def ledger_input_digest(pre, total, lens, sig, pk):
     return h16(pre[:total], lens.astype("<i4"), sig, pk)
+
+
+# ---------------------------------------------------------------- config 5, serialized blobs
+# One ledger of serialized Payment transactions: what a ledger
+# close feeds checkSign -- each transaction rebuilt from its SHAMap item's
+# bytes (/root/reference/src/ripple_app/consensus/LedgerConsensus.cpp:1947-1958
+# -> SerializedTransaction.cpp:65-92, checkSign at :220-230).  Every blob is in
+# canonical STObject::add order (SerializeDeclarations.h field codes):
+#
+#   TransactionType 12 0000 | Flags 22 80000000 | Sequence 24 .. | [DestinationTag 2E ..]
+#   | Amount 61 (native 40 00 00 + 5 B, or IOU: head + "USD" currency + issuer)
+#   | Fee 68 40..0A | SigningPubKey 73 20 <pk> | TxnSignature 74 40 <R||S>
+#   | Account 81 14 <20 B> | Destination 83 14 <20 B>
+#   | [Memos F9 { Memo EA { MemoData 7D VL <bytes> } E1 } F1]
+#
+# lengths log-uniform in [len_min, len_max] reached with the memo (a bare
+# Payment is 175-220 B, so rows drawn shorter stay bare), 1,000 signers.  2 %
+# of the rows are made invalid, five kinds in turn:
+#   0 payload_bit     a Destination bit flipped after signing   -> reject (status OK)
+#   1 R_bit / 2 S_bit a signature bit flipped after signing     -> reject (status OK)
+#   3 deferred_order  Flags and Sequence swapped after signing: the reference
+#                     re-serialises them in order, so its checkSign accepts;
+#                     the device cannot prove the form canonical -> DEFERRED
+#   4 malformed_pk33  a 33-byte SigningPubKey (signed over its own preimage)
+#                     -> checkSign false (RippleAddress.cpp:192-194), MALFORMED
+CONFIG5B = {"n": 1 << 20, "seed": 0x5EED0006, "signers": 1000, "frac": 0.02, "len_min": 100, "len_max": 4096,
+            "iou": 0.2, "tag": 0.5}
+BLOB_KINDS = ("payload_bit", "R_bit", "S_bit", "deferred_order", "malformed_pk33")
+
+
+def _put(buf, pos, data):
+    """buf[pos + j] = data[j] for a constant byte string, every row."""
+    for j, b in enumerate(data):
+        buf[pos + j] = b
+
+
+def _put_rows(buf, pos, rows):
+    """buf[pos[i] + j] = rows[i, j] (rows: (m, k) uint8), column by column."""
+    for j in range(rows.shape[1]):
+        buf[pos + j] = rows[:, j]
+
+
+def account_ids(pks):
+    """Synthetic 20-byte account ids of the signers (tests/txblob.py
+    account_id: SHA-256(pk)[:20])."""
+    return np.frombuffer(b"".join(hashlib.sha256(bytes(p)).digest()[:20] for p in pks), np.uint8).reshape(-1, 20)
+
+
+def blob_ledger_plan(signer_pks, cfg=CONFIG5B):
+    """The unsigned ledger: blob bytes with a zeroed TxnSignature slot, the
+    row layout and the invalid rows.  signer_pks(seeds (s,32)) -> (s,32): the
+    RFC 8032 public keys of the signer seeds (the device signer on the box,
+    libsodium here -- the same bytes)."""
+    rng = np.random.default_rng(cfg["seed"])
+    n = cfg["n"]
+    seeds = rng.integers(0, 256, (cfg["signers"], 32), dtype=np.uint8)
+    who = rng.integers(0, cfg["signers"], n)
+    target = np.exp(rng.uniform(np.log(cfg["len_min"]), np.log(cfg["len_max"]), n)).astype(np.int64)
+    tag = rng.random(n) < cfg["tag"]
+    iou = rng.random(n) < cfg["iou"]
+    ni = int(iou.sum())
+    mant = rng.integers(10 ** 15, 10 ** 16, ni, dtype=np.uint64)
+    expo = rng.integers(-96, 81, ni).astype(np.int64)
+    bad = np.sort(rng.choice(n, int(n * cfg["frac"]), replace=False))
+    kind = (np.arange(bad.size) % len(BLOB_KINDS)).astype(np.uint8)
+    param = rng.integers(0, 1 << 32, bad.size, dtype=np.uint64)
+    pk_len = np.full(n, 32, np.int64)
+    pk_len[bad[kind == 4]] = 33
+    p_amt = 13 + 5 * tag.astype(np.int64)
+    p_fee = p_amt + np.where(iou, 49, 9)
+    p_pk = p_fee + 9
+    p_sig = p_pk + 2 + pk_len
+    p_acc = p_sig + 66
+    p_dst = p_acc + 22
+    p_memo = p_dst + 22
+    extra = target - p_memo
+    mb = np.where(extra >= 7, np.where(extra - 6 <= 192, extra - 6, np.maximum(extra - 7, 193)), 0)
+    vlb = np.where(mb == 0, 0, np.where(mb <= 192, 1, 2))
+    lens = p_memo + np.where(mb > 0, 5 + vlb + mb, 0)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum(lens[:-1])
+    total = int(offs[-1] + lens[-1])
+    buf = rng.integers(0, 256, total + 16, dtype=np.uint8)  # value bytes; 16 B tail: the kernels' loads
+    pks = np.ascontiguousarray(signer_pks(seeds), np.uint8)
+    o = offs
+    _put(buf, o, b"\x12\x00\x00\x22\x80\x00\x00\x00\x24")
+    _put(buf, o[tag] + 13, b"\x2e")
+    _put(buf, o + p_amt, b"\x61")
+    nat = ~iou
+    _put(buf, o[nat] + p_amt[nat] + 1, b"\x40\x00\x00")
+    head = mant | ((expo + 512 + 256 + 97).astype(np.uint64) << np.uint64(54))
+    _put_rows(buf, o[iou] + p_amt[iou] + 1, head.astype(">u8").view(np.uint8).reshape(-1, 8))
+    _put(buf, o[iou] + p_amt[iou] + 9, b"\0" * 12 + b"USD" + b"\0" * 5)
+    _put(buf, o + p_fee, b"\x68\x40\x00\x00\x00\x00\x00\x00\x0a")
+    _put(buf, o + p_pk, b"\x73")
+    buf[o + p_pk + 1] = pk_len.astype(np.uint8)
+    _put_rows(buf, o + p_pk + 2, pks[who])
+    _put(buf, o + p_sig, b"\x74\x40")
+    _put_rows(buf, o + p_sig + 2, np.zeros((n, 64), np.uint8))
+    _put(buf, o + p_acc, b"\x81\x14")
+    _put_rows(buf, o + p_acc + 2, account_ids(pks)[who])
+    _put(buf, o + p_dst, b"\x83\x14")
+    m = mb > 0
+    pm = o[m] + p_memo[m]
+    _put(buf, pm, b"\xf9\xea\x7d")
+    one, two = vlb[m] == 1, vlb[m] == 2
+    buf[pm[one] + 3] = mb[m][one].astype(np.uint8)
+    v = mb[m][two] - 193
+    buf[pm[two] + 3] = (193 + (v >> 8)).astype(np.uint8)
+    buf[pm[two] + 4] = (v & 0xFF).astype(np.uint8)
+    end = pm + 3 + vlb[m] + mb[m]
+    _put(buf, end, b"\xe1\xf1")
+    return {"n": n, "buf": buf, "total": total, "offs": offs, "lens": lens.astype(np.int32), "seeds": seeds,
+            "who": who, "pks": pks, "p_sig": p_sig, "p_dst": p_dst, "bad": bad, "kind": kind, "param": param}
+
+
+def blob_signing_hashes(bp, rows=None):
+    """SHA512Half("STX\\0" || blob minus its TxnSignature field) of every row
+    (or of `rows`): the signing hash the reference computes for a canonical
+    blob (SerializedTransaction::getSigningHash -> STObject::getSigningHash,
+    SerializedObject.cpp:444-450, HashPrefix.cpp:30), hashed on the host with
+    hashlib -- independent of the device's splice."""
+    mv = memoryview(bp["buf"])
+    offs, lens, ps = bp["offs"], bp["lens"], bp["p_sig"]
+    idx = range(bp["n"]) if rows is None else rows
+    out = bytearray()
+    for i in idx:
+        o, s = int(offs[i]), int(ps[i])
+        h = hashlib.sha512(b"STX\x00")
+        h.update(mv[o:o + s])
+        h.update(mv[o + s + 66:o + int(lens[i])])
+        out += h.digest()[:32]
+    return np.frombuffer(bytes(out), np.uint8).reshape(-1, 32)
+
+
+def blob_ledger_finish(bp, sig):
+    """Write every row's signature into its TxnSignature slot, then make the
+    invalid rows (BLOB_KINDS 0-3; kind 4 is in the layout) -- in place."""
+    buf, o = bp["buf"], bp["offs"]
+    _put_rows(buf, o + bp["p_sig"] + 2, np.ascontiguousarray(sig, np.uint8))
+    bad, kind, u = bp["bad"], bp["kind"], bp["param"]
+    bit = (np.uint64(1) << ((u >> np.uint64(16)) & np.uint64(7))).astype(np.uint8)
+    r = bad
+    at = {0: o[r] + bp["p_dst"][r] + 2 + (u % np.uint64(20)).astype(np.int64),
+          1: o[r] + bp["p_sig"][r] + 2 + (u % np.uint64(32)).astype(np.int64),
+          2: o[r] + bp["p_sig"][r] + 34 + (u % np.uint64(32)).astype(np.int64)}
+    for k, pos in at.items():
+        sel = kind == k
+        buf[pos[sel]] ^= bit[sel]
+    sw = o[bad[kind == 3]]
+    a = [buf[sw + 3 + j].copy() for j in range(5)]
+    for j in range(5):
+        buf[sw + 3 + j] = buf[sw + 8 + j]
+        buf[sw + 8 + j] = a[j]
+    return bp
+
+
+def blob_ledger_inputs_h16(bp):
+    return h16(bp["buf"][:bp["total"]], bp["lens"].astype("<i4"))
+
+
+def blob_expected_status(bp):
+    """Per-row status the device contract gives this ledger by construction:
+    OK, DEFERRED (kind 3) or MALFORMED (kind 4).  make_digests.py checks it
+    against the reference re-serialiser (oracle/stl_oracle_tx.c) row by row."""
+    st = np.zeros(bp["n"], np.uint8)
+    st[bp["bad"][bp["kind"] == 3]] = 1
+    st[bp["bad"][bp["kind"] == 4]] = 2
+    return st
+
+
+def blob_ledger_cpu(oracle, n, frac=0.05, seed=0x5EED0007):
+    """A small blob ledger of the same construction, keys and signatures from
+    the CPU oracle (tests: construction and status checks on the host, the
+    config-5-size parity test on the GPU).  -> (plan, list of blob bytes)."""
+    sks = []
+
+    def pks(seeds):
+        out = []
+        for s in seeds:
+            pk, sk = oracle.keypair(bytes(s))
+            out.append(np.frombuffer(pk, np.uint8))
+            sks.append(sk)
+        return np.array(out)
+    bp = blob_ledger_plan(pks, dict(CONFIG5B, n=n, frac=frac, seed=seed))
+    msgs = blob_signing_hashes(bp)
+    sig = np.array([np.frombuffer(oracle.sign(bytes(msgs[i]), sks[w]), np.uint8) for i, w in enumerate(bp["who"])])
+    blob_ledger_finish(bp, sig)
+    buf, offs, lens = bp["buf"], bp["offs"], bp["lens"]
+    return bp, [bytes(buf[int(o):int(o) + int(ln)]) for o, ln in zip(offs, lens)]

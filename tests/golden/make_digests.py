@@ -12,7 +12,7 @@ box.  Signing and verification both go through oracle/_ref/libsodium_ref.so
 (crypto_sign_seed_keypair + crypto_sign_detached, and the reference's
 verifySignature = crypto_sign_verify_detached && S < L).
 
-    python tests/golden/make_digests.py [config2 config4 config3 config5]
+    python tests/golden/make_digests.py [config2 config4 config3 config5 config5b]
 """
 import json
 import os
@@ -80,6 +80,73 @@ def config5(lib, threads):
                              "over SHA512Half (hashlib) of each preimage"}
 
 
+def config5b(lib, threads):
+    """The serialized-blob ledger of datasets.blob_ledger_plan: signer keys and
+    signatures from libsodium over hashlib's SHA512Half of each blob's signing
+    preimage, the invalid rows made, then the reference's checkSign of every
+    row -- parse, re-serialise (oracle/stl_oracle_tx.c, the STObject::set / add
+    restatement), OpenSSL SHA-512, libsodium verify && S < L
+    (ref_tx_blob_verify_batch) -- and each row's status under the device
+    contract (include/stl.h STL_TX_*) from the same re-serialiser: DEFERRED
+    unless the blob re-serialises to itself, MALFORMED when SigningPubKey is
+    not 32 B or TxnSignature not 64 B."""
+    import ctypes
+    import hashlib
+    zeros = lambda s: oracle_bind.sodium_sign_batch(lib, s, np.zeros((s.shape[0], 32), np.uint8), threads)[0]  # noqa: E731
+    bp = datasets.blob_ledger_plan(zeros)
+    n = bp["n"]
+    msgs = datasets.blob_signing_hashes(bp)
+    pk, sig = oracle_bind.sodium_sign_batch(lib, np.ascontiguousarray(bp["seeds"][bp["who"]]), msgs, threads)
+    assert np.array_equal(pk, bp["pks"][bp["who"]])
+    datasets.blob_ledger_finish(bp, sig)
+    buf, offs, lens = bp["buf"], bp["offs"].astype(np.uint64), bp["lens"].astype(np.uint32)
+    B = oracle_bind._buf
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    ids = np.zeros((n, 32), np.uint8)
+    lib.ref_tx_blob_verify_batch(B(buf), B(offs), B(lens), n, B(bm), B(ids), 0, threads)
+    ref_bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    orc = oracle_bind.load_oracle()
+    mv = memoryview(buf)
+    status = np.zeros(n, np.uint8)
+    cap = int(lens.max()) + 64
+    sb, fb = ctypes.create_string_buffer(cap), ctypes.create_string_buffer(cap)
+    info = oracle_bind.TxInfo()
+    for i in range(n):
+        b = mv[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+        ok = orc.lib.oracle_tx_blob(b, len(b), sb, fb, cap, ctypes.byref(info)) == 0
+        assert ok, ("reference cannot construct row", i)
+        if fb.raw[:info.full_len] != b:
+            status[i] = 1
+        elif info.pk_len != 32 or info.sig_len != 64:
+            status[i] = 2
+    want_st = datasets.blob_expected_status(bp)
+    assert np.array_equal(status, want_st), np.nonzero(status != want_st)[0][:10]
+    kinds = {k: bp["bad"][bp["kind"] == i] for i, k in enumerate(datasets.BLOB_KINDS)}
+    for k in ("payload_bit", "R_bit", "S_bit", "malformed_pk33"):
+        assert not ref_bits[kinds[k]].any(), k
+    assert ref_bits[kinds["deferred_order"]].all()
+    assert ref_bits.sum() == n - bp["bad"].size + kinds["deferred_order"].size
+    dev_bits = ref_bits & (status == 0)
+    ids[status == 1] = 0  # the device writes no id for a deferred row
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    return {"rows": n, "accepted": int(dev_bits.sum()),
+            "bitmap_sha256": sha(np.packbits(dev_bits, bitorder="little")),
+            "ref_accepted": int(ref_bits.sum()), "ref_bitmap_sha256": sha(np.packbits(ref_bits, bitorder="little")),
+            "status_sha256": sha(status), "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
+            "ids_sha256": sha(ids), "inputs_h16": datasets.blob_ledger_inputs_h16(bp),
+            "blob_bytes": bp["total"], "invalid_rows": int(bp["bad"].size),
+            "invalid_by_kind": {k: int(v.size) for k, v in kinds.items()},
+            **{k: v for k, v in datasets.CONFIG5B.items()},
+            "construction": "datasets.blob_ledger_plan: one ledger of canonical serialized Payment blobs, signed "
+                            "over SHA512Half('STX\\0' || blob minus TxnSignature), invalid rows made after "
+                            "signing (datasets.BLOB_KINDS)",
+            "expected_from": f"reference checkSign per row: oracle/stl_oracle_tx.c parse + re-serialise, OpenSSL "
+                             f"SHA-512, libsodium {lib.ref_sodium_version().decode()} crypto_sign_verify_detached "
+                             "&& S < L (ref_tx_blob_verify_batch); bitmap_sha256 = that && status OK (the device "
+                             "contract: deferred and malformed rows carry accept bit 0); ids_sha256 = "
+                             "SHA512Half('TXN\\0' || blob), zero for deferred rows"}
+
+
 def main(names):
     lib = oracle_bind.load_sodium_ref()
     assert lib is not None, "needs libsodium"
@@ -91,13 +158,13 @@ def main(names):
     group = datasets.sodium_group(lib)
     for name in names:
         t0 = time.time()
-        if name == "config5":
-            got = config5(lib, threads)
+        if name in ("config5", "config5b"):
+            got = (config5 if name == "config5" else config5b)(lib, threads)
             _check_same(out, name, got)
             out[name] = got
             with open(datasets.DIGESTS, "w") as f:
                 json.dump(out, f, indent=1, sort_keys=True)
-            print(f"config5: {got['accepted']} accepted ({time.time() - t0:.0f} s)", flush=True)
+            print(f"{name}: {got['accepted']} accepted ({time.time() - t0:.0f} s)", flush=True)
             continue
         dg = datasets.Digest()
         blk = datasets.BlockDigest()
@@ -136,4 +203,4 @@ def main(names):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["config2", "config4", "config3", "config5"])
+    main(sys.argv[1:] or ["config2", "config4", "config3", "config5", "config5b"])

@@ -6,7 +6,8 @@ driver's SCALE path: per-rank shards, barriers, max-over-ranks timing, the
 digest-checked configs[2] / configs[3] / configs[4] legs (extra_configs:
 each rank rebuilds its block shard of the committed datasets, rank 0 checks
 the gathered bitmap's SHA-256 against libsodium's; config 5 is one ledger
-split by preimage bytes) and rank 0's JSON line.  The
+split by preimage bytes, and again as serialized blobs split by blob bytes,
+with status bytes and transaction ids gathered too) and rank 0's JSON line.  The
 reference parallelism this replaces is the JobQueue pool,
 src/ripple_core/functional/JobQueue.cpp:217-243."""
 import json
@@ -41,7 +42,7 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert line["stats"]["accepted"] == line["stats"]["verifies"] == 65536 * 2
     assert line["config"]["gather_check"]["slices_equal_rank_words"] is True
     extra = line["extra_configs"]
-    for key in ("config3_64M_digest", "config4_10M_digest", "config5_ledger_split"):
+    for key in ("config3_64M_digest", "config4_10M_digest", "config5_ledger_split", "config5_blob_split"):
         assert "error" not in extra[key], (key, extra[key])
     c3, c4, c5 = extra["config3_64M_digest"], extra["config4_10M_digest"], extra["config5_ledger_split"]
     assert c3["rows"] == 1 << 26 and c3["n_ranks"] == 2 and c3["digest_equal"] is True
@@ -54,3 +55,9 @@ def test_bench_two_ranks_gloo_rehearsal():
     sl = c5["small_ledgers"]
     assert sl["bits_equal_expected"] is True and sl["transactions"] == 1 << 20
     assert 1000 <= sl["ledger_size"]["median"] <= 20000 and sl["latency_ms"]["p50"] > 0
+    cb = extra["config5_blob_split"]  # serialized blobs split by bytes: bits, statuses and ids gathered
+    assert cb["n_ranks"] == 2 and cb["transactions"] == 1 << 20
+    assert cb["digest_equal"] is True and cb["digest_equal_no_dedup"] is True and cb["digest_equal_two_step"] is True
+    assert cb["status_digest_equal"] is True and cb["ids_digest_equal"] is True
+    assert cb["accepted"] == cb["accepted_expected"]
+    assert cb["byte_shards"][0][0] == 0 and cb["byte_shards"][1][1] == 1 << 20

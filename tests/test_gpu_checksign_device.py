@@ -167,3 +167,68 @@ def test_checksign_device_faults_are_errors(stl, torch_cuda, ledger, m):
         w = stl.tx_verify_batch_device(d_pre, d_off[sl], d_len[sl], sig[sl], pk[sl])
         torch.cuda.synchronize()
         assert np.array_equal(stl.words_to_bool(w, m), ref), k
+
+
+@pytest.fixture(scope="module")
+def blob_ledger(stl, torch_cuda):
+    """The config-5 ledger as serialized transactions (tests/datasets.py
+    blob_ledger_plan, 2^20 blobs): signed on the device over hashlib's signing
+    hashes, invalid rows made after signing; its input digest must equal the
+    committed one (tests/golden/make_digests.py config5b)."""
+    torch = torch_cuda
+
+    def signer_pks(seeds):
+        z = torch.zeros((seeds.shape[0], 32), dtype=torch.uint8, device="cuda")
+        return stl.sign_batch_device(torch.from_numpy(np.ascontiguousarray(seeds)).cuda(), z)[0].cpu().numpy()
+    bp = datasets.blob_ledger_plan(signer_pks)
+    msgs = torch.from_numpy(datasets.blob_signing_hashes(bp)).cuda()
+    _, sig = stl.sign_batch_device(torch.from_numpy(np.ascontiguousarray(bp["seeds"][bp["who"]])).cuda(), msgs)
+    datasets.blob_ledger_finish(bp, sig.cpu().numpy())
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)["config5b"]
+    assert datasets.blob_ledger_inputs_h16(bp) == want["inputs_h16"]
+    d = (torch.from_numpy(bp["buf"]).cuda(), torch.from_numpy(bp["offs"]).cuda(), torch.from_numpy(bp["lens"]).cuda())
+    torch.cuda.synchronize()
+    return bp, want, d
+
+
+@pytest.mark.timeout(300)
+def test_blob_ledger_digests(stl, torch_cuda, blob_ledger):
+    """the whole 2^20-blob ledger in one
+    stl_signed_blob_verify_batch_device call -- accept bits, status bytes and
+    transaction ids equal the reference's digests (re-serialise + OpenSSL +
+    libsodium per row), under each dedup choice, one stream, and the two-step
+    path; byte-balanced halves (the N = 2 shards) give the same bits."""
+    torch = torch_cuda
+    bp, want, (d_buf, d_off, d_len) = blob_ledger
+    n = bp["n"]
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    for flags in (0, stl.DEDUP_KEYS, stl.NO_AUTO_DEDUP):
+        o = stl.signed_blob_verify_batch_device(d_buf, d_off, d_len, tx_ids=True, policy=flags)
+        torch.cuda.synchronize()
+        assert _digest(stl, o["words"], n) == want["bitmap_sha256"], flags
+        assert sha(o["status"].cpu().numpy()) == want["status_sha256"], flags
+        assert sha(o["tx_id"].cpu().numpy()) == want["ids_sha256"], flags
+    old = stl.debug_tuning(stl.TUNE_STREAMS, 1)
+    try:
+        o = stl.signed_blob_verify_batch_device(d_buf, d_off, d_len)
+        torch.cuda.synchronize()
+        assert _digest(stl, o["words"], n) == want["bitmap_sha256"]
+    finally:
+        stl.debug_tuning(stl.TUNE_STREAMS, old)
+    p = stl.tx_blob_prepare_device(d_buf, d_off, d_len, tx_ids=False)
+    w = stl.verify_batch_device(p["sig"], p["msg"], p["pk"])
+    torch.cuda.synchronize()
+    assert _digest(stl, w, n) == want["bitmap_sha256"]
+    assert sha(p["status"].cpu().numpy()) == want["status_sha256"]
+    # byte shards of two ranks, concatenated
+    bits, sts = [], []
+    for r in range(2):
+        lo, hi = stl.shard_range_bytes(bp["lens"], r, 2)
+        o = stl.signed_blob_verify_batch_device(d_buf, d_off[lo:hi], d_len[lo:hi])
+        torch.cuda.synchronize()
+        bits.append(stl.words_to_bool(o["words"], hi - lo))
+        sts.append(o["status"].cpu().numpy())
+    b = np.concatenate(bits)
+    assert hashlib.sha256(np.packbits(b, bitorder="little").tobytes()).hexdigest() == want["bitmap_sha256"]
+    assert sha(np.concatenate(sts)) == want["status_sha256"]

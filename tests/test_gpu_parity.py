@@ -454,22 +454,21 @@ def test_tx_blob_prepare_device(stl, oracle, torch_cuda):
 
 
 def test_tx_blob_config5_sizes(stl, oracle):
-    """Ledger-replay shaped blobs (log-uniform 100 B - 4 KB) in one batch of
-    20,000 (SURVEY config 5 ledger size): all accepted, ids and a sample of
-    bits against the oracle."""
-    from tests import txblob as T
-    rng = np.random.default_rng(0x5EED0005)
-    ks = T.keys(oracle, 16, 3)
-    blobs = []
-    for i in range(20000):
-        pk, sk = ks[i % 16]
-        target = int(np.exp(rng.uniform(np.log(100), np.log(4096))))
-        fs = T.payment_fields(rng, pk, i + 1, pad_to=target)
-        blobs.append(T.signed_blob(fs, sk, oracle.sign)[0])
-    bits, st, ids = stl.tx_blob_verify_batch(blobs, tx_ids=True)
-    assert (st == 0).all() and bits.all()
-    for i in rng.choice(len(blobs), 500, replace=False):
-        assert bytes(ids[i]) == T.tx_id(blobs[i])
+    """Ledger-replay shaped blobs (tests/datasets.py blob_ledger_plan: log-
+    uniform 100 B - 4 KB, 2 % invalid -- payload / R / S bits flipped after
+    signing, Flags and Sequence swapped, 33-byte keys) in one batch of 20,000
+    (SURVEY config-5 ledger size): every row's bit, status and transaction id
+    against the re-serialising oracle and the device pass's host build
+    (VERDICT r4 #1: not only bits.all())."""
+    from tests import datasets as D
+    bp, blobs = D.blob_ledger_cpu(oracle, 20000, frac=0.02)
+    exp = _blob_expectations(oracle, blobs)
+    assert np.array_equal(exp["status"], D.blob_expected_status(bp))
+    for policy in (0, stl.DEDUP_KEYS):
+        bits, st, ids = stl.tx_blob_verify_batch(blobs, policy=policy, tx_ids=True)
+        _check_blob_results(bits, st, ids, exp)
+    assert (st == 1).sum() == (bp["kind"] == 3).sum() and (st == 2).sum() == (bp["kind"] == 4).sum()
+    assert bits.sum() == len(blobs) - bp["bad"].size
 
 
 def test_batcher_verdicts(stl, oracle, golden):

@@ -1,0 +1,170 @@
+"""Caller streams and libstl's per-stream contexts.
+
+stellard calls verify from many JobQueue workers at once
+(/root/reference/src/ripple_core/functional/JobQueue.cpp:217-243); a PyTorch
+user of the device-resident API brings its own streams.  Two properties:
+
+* concurrent device-resident calls on separate caller streams, mixed with host
+  batches, give exactly the bits of the same rows called alone -- the one-call
+  checkSign shares pool stream 1 (and its hash queue) between every caller
+  stream, and growing n grows those buffers while other threads launch;
+* a caller cycling through many streams does not grow device memory without
+  bound: libstl keeps at most STL_TUNE_STREAM_WORKSPACES caller contexts per
+  device (LRU), and stl_release_stream frees one.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from tests import datasets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def stl(torch_cuda):
+    from stellard_amd import verify
+    verify.init()
+    return verify
+
+
+@pytest.fixture(scope="module")
+def ledger(stl, torch_cuda):
+    """A 2^18-row ledger of the config-5 construction (tests/datasets.py:
+    'STX\\0' + random bytes, 113 B - 4 KB, 1,000 signers, 2 % of the rows with
+    a preimage / R / S bit flipped after signing): every flipped row rejects,
+    every other row accepts."""
+    torch = torch_cuda
+    lp = datasets.ledger_plan(dict(datasets.CONFIG5, n=1 << 18))
+    d_pre = torch.from_numpy(lp["pre"]).cuda()
+    d_off = torch.from_numpy(lp["offs"]).cuda()
+    d_len = torch.from_numpy(lp["lens"]).cuda()
+    seeds = torch.from_numpy(np.ascontiguousarray(lp["signers"][lp["who"]])).cuda()
+    msgs = stl.tx_hash_batch_device(d_pre, d_off, d_len)
+    pk, sig = stl.sign_batch_device(seeds, msgs)
+    (pos, pbit), (srow, scol, sbit) = datasets.ledger_mutations(lp)
+    d_pre[torch.from_numpy(pos).cuda()] ^= torch.from_numpy(pbit).cuda()
+    sig[torch.from_numpy(srow).cuda(), torch.from_numpy(scol).cuda()] ^= torch.from_numpy(sbit).cuda()
+    msgs = stl.tx_hash_batch_device(d_pre, d_off, d_len)  # the signing hashes of the mutated preimages
+    torch.cuda.synchronize()
+    expect = np.ones(lp["n"], dtype=bool)
+    expect[lp["bad"]] = False
+    return lp, d_pre, d_off, d_len, sig, pk, msgs, expect
+
+
+@pytest.mark.timeout(300)
+def test_concurrent_calls_on_caller_streams(stl, torch_cuda, ledger):
+    """Four threads at once, each on its own stream, sizes growing and
+    shrinking so that the shared pool stream's workspace and hash queue grow
+    while other threads launch: one-call checkSign from preimages (two
+    threads), device-resident verify of the signing hashes, and the host
+    batch API -- every call's bits equal the plan's."""
+    torch = torch_cuda
+    lp, d_pre, d_off, d_len, sig, pk, msgs, expect = ledger
+    n = lp["n"]
+    h_pre, h_off, h_len = lp["pre"], lp["offs"].astype(np.uint64), lp["lens"].astype(np.uint32)
+    h_sig, h_pk = sig.cpu().numpy(), pk.cpu().numpy()
+    errors = []
+
+    def rows(k, m):
+        lo = (k * 7919 * 64) % (n - m + 1) // 64 * 64
+        return lo, lo + m
+
+    def device_checksign(tid):
+        st = torch.cuda.Stream()
+        for k, m in enumerate((1_000, 20_000, 100_000, n, 5_000, 150_001, n - 64)):
+            lo, hi = rows(k + tid, m)
+            with torch.cuda.stream(st):
+                w = stl.tx_verify_batch_device(d_pre, d_off[lo:hi], d_len[lo:hi], sig[lo:hi], pk[lo:hi], stream=st)
+            st.synchronize()
+            if not np.array_equal(stl.words_to_bool(w, m), expect[lo:hi]):
+                errors.append(("checksign", tid, lo, m))
+
+    def device_verify(tid):
+        st = torch.cuda.Stream()
+        for k, m in enumerate((64, 30_000, n, 70_001, 200_000, 3)):
+            lo, hi = rows(k + tid, m)
+            with torch.cuda.stream(st):
+                w = stl.verify_batch_device(sig[lo:hi], msgs[lo:hi], pk[lo:hi], stream=st)
+            st.synchronize()
+            if not np.array_equal(stl.words_to_bool(w, m), expect[lo:hi]):
+                errors.append(("verify", tid, lo, m))
+
+    def host_batches(tid):
+        for k, m in enumerate((4_000, 131_072, 9_999)):
+            lo, hi = rows(k + tid, m)
+            pres = [bytes(h_pre[int(h_off[i]):int(h_off[i]) + int(h_len[i])]) for i in range(lo, hi)]
+            bits = stl.tx_verify_batch(pres, h_sig[lo:hi], h_pk[lo:hi])
+            if not np.array_equal(np.asarray(bits, bool), expect[lo:hi]):
+                errors.append(("host", tid, lo, m))
+
+    th = [threading.Thread(target=f, args=(t,)) for t, f in
+          enumerate((device_checksign, device_checksign, device_verify, host_batches))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+
+
+@pytest.mark.timeout(300)
+def test_caller_stream_contexts_are_capped(stl, torch_cuda):
+    """1M-signature launches on eight caller streams in turn under a cap of
+    three contexts: the number of caller contexts and the device memory in use
+    stop growing at the cap, every launch accepts all 1,048,576 signatures,
+    and stl_release_stream frees a context."""
+    torch = torch_cuda
+    n = 1 << 20
+    rng = np.random.default_rng(0x57AB)
+    seeds = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+    pk, sig = stl.sign_batch_device(seeds, msgs)
+    torch.cuda.synchronize()
+    old = stl.debug_tuning(stl.TUNE_STREAM_WORKSPACES, 3)
+    streams = []
+    try:
+        base = stl.stream_contexts()
+        used, ctxs = [], []
+        for k in range(8):
+            st = torch.cuda.Stream()
+            streams.append(st)
+            with torch.cuda.stream(st):
+                w = stl.verify_batch_device(sig, msgs, pk, stream=st)
+            st.synchronize()
+            assert stl.words_to_bool(w, n).all(), k
+            del w
+            torch.cuda.synchronize()
+            free, total = torch.cuda.mem_get_info()
+            used.append(total - free)
+            ctxs.append(stl.stream_contexts())
+        assert max(ctxs) <= 3, ctxs
+        assert ctxs[-1] == 3 or base > 3, ctxs
+        # memory: from the third stream on (the cap reached) no further growth
+        # beyond allocator noise
+        assert max(used[2:]) <= used[2] + (64 << 20), [u >> 20 for u in used]
+        before = stl.stream_contexts()
+        stl.release_stream(streams[-1])
+        assert stl.stream_contexts() == before - 1
+        stl.release_stream(streams[-1])  # a second release finds none: still OK
+        # the released stream works again (a fresh context)
+        with torch.cuda.stream(streams[-1]):
+            w = stl.verify_batch_device(sig, msgs, pk, stream=streams[-1])
+        streams[-1].synchronize()
+        assert stl.words_to_bool(w, n).all()
+    finally:
+        stl.debug_tuning(stl.TUNE_STREAM_WORKSPACES, old)
+        for st in streams:
+            stl.release_stream(st)
+        torch.cuda.synchronize()

@@ -284,3 +284,41 @@ def test_txnsignatures_always_deferred(oracle, emu):
     assert hostemu_tx_blob(emu, blob)[0] == DEFERRED
     assert hostemu_signed_blob(emu, 0, blob)[0] == DEFERRED
     assert hostemu_signed_blob(emu, 1, blob)[0] == DEFERRED
+
+
+def test_blob_ledger_construction(oracle, emu):
+    """The config-5 blob ledger's construction (tests/datasets.py
+    blob_ledger_plan, here 3,000 rows with 5 % invalid): every row is built
+    by the reference re-serialiser; canonical rows re-serialise to themselves
+    and their signing preimage hashes to the construction's signing hash;
+    the statuses by the reference's rules equal the construction's
+    (deferred = Flags / Sequence swapped, malformed = 33-byte key) and the
+    device pass's on the host; the reference accepts exactly the honest and
+    the deferred rows."""
+    from tests import datasets as D
+    bp, blobs = D.blob_ledger_cpu(oracle, 3000)
+    want = D.blob_expected_status(bp)
+    msgs = D.blob_signing_hashes(bp)
+    kinds = {k: set(bp["bad"][bp["kind"] == i].tolist()) for i, k in enumerate(D.BLOB_KINDS)}
+    assert all(len(v) >= 25 for v in kinds.values())
+    ref_st = np.zeros(len(blobs), np.uint8)
+    for i, b in enumerate(blobs):
+        ok, info, signing, full = oracle.tx_blob(b)
+        assert ok, i
+        if full != b:
+            ref_st[i] = DEFERRED
+        elif info.pk_len != 32 or info.sig_len != 64:
+            ref_st[i] = MALFORMED
+        else:
+            assert h512half(signing) == bytes(msgs[i]) or i in kinds["payload_bit"], i
+        st, msg, tid, _ = hostemu_tx_blob(emu, b)
+        assert st == want[i], (i, st, want[i])
+        if st == OK:
+            assert msg == h512half(signing) and tid == T.tx_id(b)
+    assert np.array_equal(ref_st, want)
+    bits = oracle.tx_blob_verify_batch(blobs)
+    expect = np.ones(len(blobs), bool)
+    for k in ("payload_bit", "R_bit", "S_bit", "malformed_pk33"):
+        expect[list(kinds[k])] = False
+    assert np.array_equal(bits, expect)
+    assert 100 <= min(bp["lens"]) and max(bp["lens"]) <= 4100

@@ -15,7 +15,12 @@ the *gathered* result, not only of each rank's own slice:
   config5_ledger_split     configs[4]: ONE ledger of 2^20 signed preimages
                            (113 B - 4 KB, 1,000 signers, 2 % invalid rows) split
                            by preimage bytes (stl_shard_range_bytes), SHA512Half +
-                           verify per rank, stl_bitmap_gatherv_device.
+                           verify per rank, stl_bitmap_gatherv_device;
+  config5_blob_split       configs[4] from serialized transactions: ONE ledger of
+                           2^20 canonical Payment blobs (100 B - 4 KB, 2 % invalid,
+                           deferred and malformed rows) split by blob bytes,
+                           stl_signed_blob_verify_batch_device per rank, accept
+                           words and status bytes gathered, both digests checked.
 
 Every rank rebuilds only its own rows (the device signer and adversarial-row
 builder, stl_debug_sign_adversarial_device, from the seeded plans), checks its
@@ -159,6 +164,17 @@ class _BlockInputs:
         return [f.result() for f in self.futs]
 
 
+def _gather_label(ctx, offs):
+    """How the leg's bitmap slices reached rank 0 (the gloo
+    rehearsal is not labelled as RCCL)."""
+    equal = len(set(np.diff(offs.astype(np.int64)).tolist())) == 1
+    if ctx["world"] == 1:
+        return "one rank: no gather"
+    if ctx["gather"].mode == "rccl":
+        return "equal: ncclGather" if equal else "unequal: grouped send/recv (stl_bitmap_gatherv_device)"
+    return ("equal" if equal else "unequal") + f": {ctx['gather'].mode} through host memory (not RCCL)"
+
+
 def digest_leg(ctx, name, reps=3):
     """configs[2] / configs[3] on this rank's block shard; see the module
     docstring.  ctx: world, rank, dist, V, torch, dev, stream, sync, gather."""
@@ -222,9 +238,7 @@ def digest_leg(ctx, name, reps=3):
     slices = _all(ctx["dist"], world, {"rank": rank, "rows": [lo, hi], "slice_bitmap_blocks_equal": bool(slice_ok),
                                        "accepted": int(bits.sum())})
     out = {"rows": n, "n_ranks": world, "verifies_per_s": n / dt, "ms": dt * 1e3, "median_of": reps,
-           "shards": "whole 65,536-row blocks per rank (datasets.block_shard), "
-                     + ("equal: ncclGather" if len(set(np.diff(offs.astype(np.int64)))) == 1 or world == 1
-                        else "unequal: grouped send/recv (stl_bitmap_gatherv_device)"),
+           "shards": "whole 65,536-row blocks per rank (datasets.block_shard), " + _gather_label(ctx, offs),
            "rank_slices": slices, "build_s": build_s,
            "data": "tests/datasets.py %s, rows rebuilt per rank by the device signer + adversarial-row builder, "
                    "inputs checked per 65,536-row block against libsodium-built digests" % name,
@@ -323,6 +337,128 @@ def ledger_leg(ctx, reps=5):
     if rank == 0:
         out.update({"accepted_expected": want["accepted"], "bitmap_sha256_expected": want["bitmap_sha256"]})
     out["small_ledgers"] = small
+    return out
+
+
+def blob_ledger_leg(ctx, reps=5):
+    """configs[4] as a ledger close feeds it: ONE ledger of
+    2^20 serialized Payment transactions (tests/datasets.py blob_ledger_plan:
+    canonical blobs memo-padded to log-uniform 100 B - 4 KB, 1,000 signers, 2 %
+    invalid -- payload / R / S bits flipped after signing, Flags and Sequence
+    swapped (deferred), 33-byte keys (malformed)) split by blob bytes
+    (stl_shard_range_bytes); each rank runs stl_signed_blob_verify_batch_device
+    over its shard -- the canonical-form walk, TxFormats check, splice,
+    SHA512Half and verify -- and the accept words and per-row status bytes are
+    gathered to rank 0 (stl_bitmap_gatherv_device), which compares their
+    SHA-256 with the committed reference digests (tests/golden/make_digests.py
+    config5b: re-serialise + OpenSSL + libsodium per row).  The reference path
+    replaced: LedgerConsensus.cpp:1947-1958 -> SerializedTransaction.cpp:65-92,
+    220-230."""
+    torch, V, dev, stream = ctx["torch"], ctx["V"], ctx["dev"], ctx["stream"]
+    world, rank = ctx["world"], ctx["rank"]
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)["config5b"]
+    err, inputs = None, None
+    try:
+        t0 = time.time()
+
+        def signer_pks(seeds):
+            z = torch.zeros((seeds.shape[0], 32), dtype=torch.uint8, device=dev)
+            return V.sign_batch_device(torch.from_numpy(np.ascontiguousarray(seeds)).to(dev), z)[0].cpu().numpy()
+        bp = datasets.blob_ledger_plan(signer_pks)
+        n = bp["n"]
+        msgs = torch.from_numpy(datasets.blob_signing_hashes(bp)).to(dev)
+        _, sig = V.sign_batch_device(torch.from_numpy(np.ascontiguousarray(bp["seeds"][bp["who"]])).to(dev), msgs)
+        datasets.blob_ledger_finish(bp, sig.cpu().numpy())
+        inputs = datasets.blob_ledger_inputs_h16(bp)
+        build_s = time.time() - t0
+        d_buf = torch.from_numpy(bp["buf"]).to(dev)
+        d_off = torch.from_numpy(bp["offs"]).to(dev)
+        d_len = torch.from_numpy(bp["lens"]).to(dev)
+        bounds = [V.shard_range_bytes(bp["lens"], r, world) for r in range(world)]
+        lo, hi = bounds[rank]
+        m = hi - lo
+        offs = np.array([b[0] // 64 for b in bounds] + [(n + 63) // 64], np.uint64)
+        words = torch.zeros((m + 63) // 64, dtype=torch.int64, device=dev)
+        # status bytes and ids ride the same gatherv as int64 words: shards
+        # start on 64-row boundaries, so a rank's status bytes are whole words
+        status = torch.zeros(((m + 63) // 64) * 64, dtype=torch.uint8, device=dev)
+        ids = torch.zeros((max(m, 1), 32), dtype=torch.uint8, device=dev)
+        full, full_st, full_id = None, None, None
+        if rank == 0:
+            full = torch.zeros(int(offs[-1]), dtype=torch.int64, device=dev)
+            full_st = torch.zeros(int(offs[-1]) * 8, dtype=torch.int64, device=dev)
+            full_id = torch.zeros(n * 4, dtype=torch.int64, device=dev)
+            if world > 1 and ctx["gather"].mode == "gloo":
+                full, full_st, full_id = full.cpu(), full_st.cpu(), full_id.cpu()
+    except Exception as e:  # noqa: BLE001 - every rank learns of it before the leg's collectives
+        err = f"rank {rank}: {e!r}"
+    st = _all(ctx["dist"], world, (err, inputs == want["inputs_h16"]))
+    if any(e for e, _ in st):
+        return {"error": "; ".join(e for e, _ in st if e)}
+    if not all(o for _, o in st):
+        return {"error": f"blob ledger input digest differs on ranks {[r for r, (_, o) in enumerate(st) if not o]}"}
+
+    def step(flags=0, fused=True):
+        if m and fused:  # one call: blob pass and verify chunk by chunk over two streams
+            V.signed_blob_verify_batch_device(d_buf, d_off[lo:hi], d_len[lo:hi], out_words=words,
+                                              out_status=status, policy=flags, stream=stream)
+        elif m:
+            o = V.tx_blob_prepare_device(d_buf, d_off[lo:hi], d_len[lo:hi], tx_ids=False, stream=stream)
+            V.verify_batch_device(o["sig"], o["msg"], o["pk"], out_words=words, policy=flags, stream=stream)
+        ctx["gather"](words, offs, full)
+
+    step()  # warm: workspaces, and the key sample the automatic dedup follows
+    ctx["sync"]()
+    res = {}
+    for label, flags in (("", 0), ("_no_dedup", V.NO_AUTO_DEDUP)):
+        dt = timed(ctx, lambda: step(flags), reps)  # noqa: B023 - called right here
+        res["tx_per_s" + label] = n / dt
+        res["ms" + label] = dt * 1e3
+        if rank == 0:
+            res["digest_equal" + label] = bitmap_sha256(full, n) == want["bitmap_sha256"]
+    dt = timed(ctx, lambda: step(0, fused=False), reps)
+    res["tx_per_s_two_step"] = n / dt
+    if rank == 0:
+        res["digest_equal_two_step"] = bitmap_sha256(full, n) == want["bitmap_sha256"]
+    # untimed: one call with transaction ids, then status bytes and ids gathered
+    if m:
+        V.signed_blob_verify_batch_device(d_buf, d_off[lo:hi], d_len[lo:hi], out_words=words, out_status=status,
+                                          out_ids=ids, stream=stream)
+    ctx["sync"]()
+    ctx["gather"](status.view(torch.int64), offs * 8, full_st)
+    ctx["gather"](ids[:m].reshape(-1).view(torch.int64) if m else ids.reshape(-1).view(torch.int64)[:0],
+                  np.array([b[0] * 4 for b in bounds] + [n * 4], np.uint64), full_id)
+    ctx["sync"]()
+    out = {"transactions": n, "n_ranks": world, "scaling": "strong (one ledger split across the ranks)",
+           "blob_bytes": bp["total"], "byte_shards": [list(map(int, b)) for b in bounds],
+           "blob_bytes_per_rank": [int(bp["offs"][b[1] - 1] + bp["lens"][b[1] - 1] - bp["offs"][b[0]])
+                                   if b[1] > b[0] else 0 for b in bounds],
+           "median_of": reps, "build_s": build_s, **res,
+           "invalid_rows": int(bp["bad"].size),
+           "invalid_by_kind": want.get("invalid_by_kind"),
+           "data": "tests/datasets.py blob_ledger_plan: canonical serialized Payment blobs (TransactionType .. "
+                   "Destination, optional DestinationTag / IOU Amount, Memos padding to log-uniform 100 B - 4 KB), "
+                   "1,000 signers, GPU-signed over hashlib SHA512Half of each signing preimage; 2 % invalid "
+                   "(payload / R / S bit flips, Flags-Sequence swap -> deferred, 33-byte key -> malformed); every "
+                   "rank builds the whole ledger and checks its input digest",
+           "timing": "barrier, stl_signed_blob_verify_batch_device over the rank's byte shard (blob pass + verify "
+                     "in one call; tx_per_s_two_step: stl_tx_blob_prepare_device then verify_batch_device) + "
+                     "gather of the accept words to rank 0 (stl_bitmap_gatherv_device), sync, barrier; median, max "
+                     "over ranks; status bytes and transaction ids gathered after the timed reps"}
+    if rank == 0:
+        stb = full_st.cpu().numpy().astype("<i8").view(np.uint8)[:n]
+        idb = full_id.cpu().numpy().astype("<i8").view(np.uint8)[:n * 32]
+        out.update({"accepted": int(np.unpackbits(full.cpu().numpy().astype("<i8").view(np.uint8),
+                                                  bitorder="little")[:n].sum()),
+                    "accepted_expected": want["accepted"], "bitmap_sha256_expected": want["bitmap_sha256"],
+                    "status_counts": {str(k): int((stb == k).sum()) for k in (0, 1, 2)},
+                    "status_digest_equal": hashlib.sha256(stb.tobytes()).hexdigest() == want["status_sha256"],
+                    "ids_digest_equal": hashlib.sha256(idb.tobytes()).hexdigest() == want["ids_sha256"],
+                    "deferred_rows_reference_accepts": "every deferred row (Flags/Sequence swapped) is accepted by "
+                                                       "the reference's re-serialising checkSign -- the caller's "
+                                                       "serial check answers them (STL_TX_DEFERRED)",
+                    "expected_from": want.get("expected_from")})
     return out
 
 
