@@ -190,6 +190,10 @@ static int field_declared(int type, int name) {
   return 0;
 }
 
+/* SField::notSigningField (FieldNames.cpp:49-51): TxnSignature, TxnSignatures,
+ * Signature are left out of STObject::add(s, false). */
+static int non_signing(uint32_t code) { return code == 0x70004u || code == 0x70006u || code == 0xF0003u; }
+
 static int type_known(int type) { return (type >= 1 && type <= 8) || (type >= 14 && type <= 19); }
 
 /* SField::getField(type, name) (FieldNames.cpp:76-111): declared fields, or a
@@ -451,7 +455,7 @@ static int parse_object(rd_t *r, int depth, flist_t *out) {
     fld_t *f = &out->f[out->n];
     memset(f, 0, sizeof *f);
     f->code = ((uint32_t)type << 16) | (uint32_t)name;
-    f->signing = !(f->code == 0x70004u || f->code == 0x70006u || f->code == 0xF0003u);
+    f->signing = !non_signing(f->code);
     put_field_id(&f->ser, type, name);
     out->n++;
     parse_value(r, type, depth, &out->f[out->n - 1].ser);
@@ -708,4 +712,32 @@ void KIND_BATCH_NAME(uint32_t kind, const uint8_t *blobs, const uint64_t *offset
   for (size_t i = 0; i < n; ++i)
     if (bits[i]) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
   free(bits);
+}
+
+/* ---- table accessors (tests/test_sfields.py pins them to the reference's
+ * own text, tests/golden/sfields.json) ---- */
+int oracle_table_declared(int type, int name) { return field_declared(type, name); }
+int oracle_table_non_signing(uint32_t code) { return non_signing(code); }
+
+/* The TxFormats template of TxType `type`: common fields then the type's own,
+ * (code, SOE flag 0 required / 1 optional / 2 default); the count, or -1 for a
+ * type with no format. */
+int oracle_table_tx_format(int type, uint32_t *codes, int *flags, int cap) {
+  const txformat_t *fmt = NULL;
+  for (size_t i = 0; i < sizeof kTxFormats / sizeof kTxFormats[0]; ++i)
+    if (kTxFormats[i].type == type) fmt = &kTxFormats[i];
+  if (!fmt) return -1;
+  int k = 0;
+  for (size_t i = 0; i < sizeof kCommonFields / sizeof kCommonFields[0]; ++i, ++k)
+    if (k < cap) codes[k] = kCommonFields[i].code, flags[k] = kCommonFields[i].flags;
+  for (int i = 0; i < fmt->n; ++i, ++k)
+    if (k < cap) codes[k] = fmt->f[i].code, flags[k] = fmt->f[i].flags;
+  return k;
+}
+
+/* SerializedValidation's template codes; the count. */
+int oracle_table_validation(uint32_t *codes, int cap) {
+  const int n = (int)(sizeof kValidationFields / sizeof kValidationFields[0]);
+  for (int i = 0; i < n && i < cap; ++i) codes[i] = kValidationFields[i];
+  return n;
 }

@@ -73,6 +73,12 @@ constexpr uint32_t kCodeTxnSignatures = 0xF0003u;  // ARRAY 3
 constexpr uint32_t kCodeObjectEnd = 0xE0001u;      // STI_OBJECT, 1
 constexpr uint32_t kCodeArrayEnd = 0xF0001u;       // STI_ARRAY, 1
 
+// SField::notSigningField (FieldNames.cpp:49-51): left out of every signing
+// hash (STObject::add(s, false)), cut out of the blob by the splice.
+STL_HD bool non_signing_field(uint32_t code) {
+  return code == kCodeTxnSignature || code == kCodeSignature || code == kCodeTxnSignatures;
+}
+
 // Which signed object a blob is (include/stl.h STL_BLOB_*): the signing-hash
 // prefix, the field that holds the signature, and the ID hash.
 struct BlobKind {
@@ -326,8 +332,7 @@ STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t, uint32_t 
     } else if (depth == 0 && format == kFormatValidation && !validation_field(code)) {
       foreign = true;
     }
-    const bool cut =
-        depth == 0 && (code == kCodeTxnSignature || code == kCodeSignature || code == kCodeTxnSignatures);
+    const bool cut = depth == 0 && non_signing_field(code);
     if (cut) {
       // strictly ascending codes: each of the three at most once
       if (ncut == 0) t.xs0 = hpos;

@@ -441,3 +441,15 @@ void hostemu_sign_adversarial(const uint8_t* seed, const uint8_t* msg, const uin
   for (auto& x : th) x.join();
 }
 }
+
+// ---- the device pass's field tables (tests/test_sfields.py pins them to the
+// reference's own text, tests/golden/sfields.json) ----
+extern "C" {
+int hostemu_tx_field_bit(uint32_t code) { return stl::tx_field_bit(code); }
+int hostemu_tx_format(uint32_t type, uint64_t* allowed, uint64_t* required) {
+  return stl::tx_format(type, *allowed, *required) ? 1 : 0;
+}
+uint64_t hostemu_declared_names(uint32_t type) { return stl::declared_names(type); }
+int hostemu_validation_field(uint32_t code) { return stl::validation_field(code) ? 1 : 0; }
+int hostemu_non_signing_field(uint32_t code) { return stl::non_signing_field(code) ? 1 : 0; }
+}
