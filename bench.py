@@ -50,6 +50,15 @@ sys.path.insert(0, ROOT)
 # ref10 operation counts N_M = 1520, N_S = 1525 measured by instrumenting the
 # oracle's restatement of libsodium's verify (oracle_op_counts), B_k = 1.
 W_VERIFY = 64 * 1520 + 36 * 1525 + 5520
+# The same work split over the two kernels that do it: phase 1
+# (verify_prep_kernel) hashes the one SHA-512 block (5,520) and decompresses A
+# and R -- each ge_frombytes_negate_vartime is 19 M + 255 S (oracle op counts,
+# tests/test_oracle_golden.py pins them); the second decompression stands in
+# for ref10's final inversion (ge_tobytes: 11 M + 254 S), which the half-size
+# check never computes.  The main kernel (the Straus loop) gets the rest.
+DECODE_OPS = 64 * 19 + 36 * 255
+W_PREP = 5520 + 2 * DECODE_OPS
+W_MAIN = W_VERIFY - W_PREP
 # gfx950 full-rate 32-bit VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 PEAK_INT_OPS = 256 * 4 * 32 * 2.4e9
 HBM_PEAK_GBS = 8000.0
@@ -186,6 +195,23 @@ def cpu_baseline(sig, msg, pk, threads_share, reps):
                       f"{threads_share}, stellard's JobQueue default 6, one thread), median of {reps} runs each; "
                       f"{what}",
             "cpu_quota": quota, "by_threads": rates, "host_nproc": os.cpu_count(), "host_affinity_cpus": avail}
+
+
+def per_kernel(vd, n, kernels):
+    """roofline.per_kernel: each kernel's share of the work model over its own
+    phase-clock time, with its PMC VALUBusy and instruction-issue bound
+    (profiles/valu_latest.json, tools/summarize_valu.py) when present."""
+    out = {}
+    for name, (work, ms) in kernels.items():
+        ach = work * n / (ms * 1e-3) if ms > 0 else 0.0
+        k = next((v for kk, v in vd.get("kernels", {}).items() if name in kk), {})
+        ib = k.get("issue_bound_ms")
+        out[name] = {"work_per_verify": work, "kernel_ms": ms, "achieved": ach / 1e12, "unit": "Tops/s",
+                     "frac": ach / PEAK_INT_OPS, "issue_bound_ms": ib,
+                     "frac_of_issue_bound": ib / ms if ib and ms > 0 else None,
+                     "valu_busy_pct": k.get("VALUBusy"),
+                     "valu_insts_per_verify": k["SQ_INSTS_VALU"] * 64 / n if k.get("SQ_INSTS_VALU") else None}
+    return out
 
 
 def end_to_end(V, torch, sig, msgs, pk, reps=5):
@@ -590,7 +616,8 @@ def gpu_run(args, world, rank, local):
         # the dominant kernel (verify_main_kernel): algorithmic work of one
         # launch (W_VERIFY x n) / its average duration, live HIP events
         main_ms = phase_ms["main"]
-        achieved = W_VERIFY * n / (main_ms * 1e-3) / 1e12
+        prep_ms = phase_ms["phase1"]
+        achieved = W_MAIN * n / (main_ms * 1e-3) / 1e12
         achieved_launch = W_VERIFY * per_launch / 1e12
         traffic, traffic_build = None, None
         from stellard_amd.build import source_digest
@@ -607,7 +634,7 @@ def gpu_run(args, world, rank, local):
                 td = json.load(f)
             traffic = (td.get("main_kernel") or {}).get("hbm_bytes_per_launch")
             traffic_build = provenance(td, tp)
-        valu_busy, issue = None, None
+        valu_busy, issue, vd = None, None, {}
         vp = os.path.join(ROOT, "profiles", "valu_latest.json")
         if os.path.exists(vp):
             with open(vp) as f:
@@ -653,15 +680,21 @@ def gpu_run(args, world, rank, local):
                                                              "another (e.g. streams sharing a hardware queue)"})},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_INT_OPS / 1e12, "unit": "Tops/s",
                          "frac": achieved * 1e12 / PEAK_INT_OPS, "traffic": traffic,
+                         "per_kernel": per_kernel(vd, n, {"verify_prep_kernel": (W_PREP, prep_ms),
+                                                          "verify_main_kernel": (W_MAIN, main_ms)}),
                          "algorithmic_bytes": BYTES_PER_VERIFY * n,
                          "traffic_over_algorithmic": traffic / (BYTES_PER_VERIFY * n) if traffic else None,
                          "traffic_build": traffic_build, "sources_sha256": digest,
                          "kernel": "verify_main_kernel (dominant: %.0f %% of the launch)"
                                    % (100.0 * main_ms / max(1e-9, sum(phase_ms.values()))),
-                         "kernel_ms": main_ms, "work_per_verify": W_VERIFY, "units_per_launch": n,
+                         "kernel_ms": main_ms, "work_per_verify": W_MAIN, "units_per_launch": n,
+                         "work_model": "W_VERIFY = 64*1520 M + 36*1525 S + 5520 (ref10 verify) = %d ops; main "
+                                       "kernel W_MAIN = W_VERIFY - W_PREP = %d, prep W_PREP = SHA-512 block + two "
+                                       "decompressions = %d" % (W_VERIFY, W_MAIN, W_PREP),
                          "timing": "libstl phase events (stl_set_phase_timing) on the launch stream over K "
                                    "launches right after the timed region (kernels one after another); work = "
-                                   "W_VERIFY x n per launch attributed to the main kernel",
+                                   "W_MAIN x n per launch, the part of W_VERIFY the main kernel does",
+                         "frac_all_work_on_main": W_VERIFY * n / (main_ms * 1e-3) / PEAK_INT_OPS,
                          "phase_ms": phase_ms,
                          "launch_ms": kern_ms, "achieved_launch": achieved_launch,
                          "frac_launch": achieved_launch * 1e12 / PEAK_INT_OPS,

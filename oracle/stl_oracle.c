@@ -757,6 +757,18 @@ int oracle_verify(const uint8_t sig[64], const uint8_t *m, size_t mlen, const ui
   return (v && canon) ? 0 : -1;
 }
 
+/* Field operations of one ge_frombytes_negate_vartime (bench.py DECODE_OPS:
+ * the work model's per-kernel split).  Returns the decoder's result. */
+int oracle_decode_op_counts(const uint8_t pk[32], uint64_t *muls, uint64_t *sqs) {
+  ensure_init();
+  ge_p3 A;
+  g_muls = g_sqs = 0;
+  const int rc = ge_frombytes_negate_vartime(&A, pk);
+  *muls = g_muls;
+  *sqs = g_sqs;
+  return rc;
+}
+
 void oracle_op_counts(uint64_t *muls, uint64_t *sqs) {
   *muls = g_last_muls;
   *sqs = g_last_sqs;

@@ -102,6 +102,7 @@ void oracle_signed_blob_verify_batch(uint32_t kind, const uint8_t *blobs, const 
 /* Instrumentation: field multiplications / squarings executed by the last
  * single-threaded oracle_verify call (for the frozen work model). */
 void oracle_op_counts(uint64_t *muls, uint64_t *sqs);
+int oracle_decode_op_counts(const uint8_t pk[32], uint64_t *muls, uint64_t *sqs);
 
 #ifdef __cplusplus
 }

@@ -541,7 +541,7 @@ bool is_pool_stream(const Device& d, hipStream_t s) {
 // caller context; the evicted one is destroyed (device sync + free) outside
 // ws_mu, once its last user has let go.
 std::shared_ptr<StreamCtx> stream_ctx(Device& d, hipStream_t s) {
-  std::shared_ptr<StreamCtx> evicted;
+  std::vector<std::shared_ptr<StreamCtx>> evicted;
   std::shared_ptr<StreamCtx> out;
   {
     std::lock_guard<std::mutex> lk(d.ws_mu);
@@ -551,23 +551,24 @@ std::shared_ptr<StreamCtx> stream_ctx(Device& d, hipStream_t s) {
       slot->ordinal = d.ordinal;
       slot->pool = is_pool_stream(d, s);
       if (!slot->pool) {
-        int callers = 0;
-        auto lru = d.stream_ws.end();
-        for (auto it = d.stream_ws.begin(); it != d.stream_ws.end(); ++it) {
-          if (it->second->pool) continue;
-          ++callers;
-          if (it->first != s && (lru == d.stream_ws.end() || it->second->last_use < lru->second->last_use)) lru = it;
-        }
-        if (callers > g_max_caller_streams.load() && lru != d.stream_ws.end()) {
-          evicted = std::move(lru->second);
-          d.stream_ws.erase(lru);
+        // the least recently used caller contexts beyond the cap (the cap
+        // may have been lowered since they were made)
+        std::vector<std::pair<uint64_t, hipStream_t>> callers;
+        for (auto& kv : d.stream_ws)
+          if (!kv.second->pool && kv.first != s) callers.emplace_back(kv.second->last_use, kv.first);
+        std::sort(callers.begin(), callers.end());
+        const size_t keep = (size_t)std::max(0, g_max_caller_streams.load() - 1);  // plus s
+        for (size_t i = 0; i + keep < callers.size(); ++i) {
+          auto it = d.stream_ws.find(callers[i].second);
+          evicted.push_back(std::move(it->second));
+          d.stream_ws.erase(it);
         }
       }
     }
-    d.stream_ws[s]->last_use = ++d.ws_tick;
     out = d.stream_ws[s];
+    out->last_use = ++d.ws_tick;
   }
-  return out;  // `evicted` (if any) is destroyed here, without ws_mu
+  return out;  // evicted contexts are destroyed here, without ws_mu
 }
 
 // Caller contexts currently kept on device d (tests: the cap holds).

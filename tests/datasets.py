@@ -490,7 +490,7 @@ def blob_signing_hashes(bp, rows=None):
         h.update(mv[o:o + s])
         h.update(mv[o + s + 66:o + int(lens[i])])
         out += h.digest()[:32]
-    return np.frombuffer(bytes(out), np.uint8).reshape(-1, 32)
+    return np.frombuffer(out, np.uint8).reshape(-1, 32)  # a writable view of the bytearray
 
 
 def blob_ledger_finish(bp, sig):

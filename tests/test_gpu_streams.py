@@ -73,7 +73,8 @@ def test_concurrent_calls_on_caller_streams(stl, torch_cuda, ledger):
     torch = torch_cuda
     lp, d_pre, d_off, d_len, sig, pk, msgs, expect = ledger
     n = lp["n"]
-    h_pre, h_off, h_len = lp["pre"], lp["offs"].astype(np.uint64), lp["lens"].astype(np.uint32)
+    # the preimages as mutated on the device (the plan's host copy is unmutated)
+    h_pre, h_off, h_len = d_pre.cpu().numpy(), lp["offs"].astype(np.uint64), lp["lens"].astype(np.uint32)
     h_sig, h_pk = sig.cpu().numpy(), pk.cpu().numpy()
     errors = []
 

@@ -132,3 +132,34 @@ def test_signatures_match_libsodium():
         sig = ctypes.create_string_buffer(64)
         ref.ref_sign_detached(sig, msg, len(msg), sk)
         assert sig.raw == o.sign(msg, s1)
+
+
+def test_work_model_op_counts(oracle):
+    """bench.py's frozen work model (DESIGN.md section 5) against the oracle's
+    own field-operation counts: a verify averages N_M = 1,520 multiplications
+    and N_S = 1,525 squarings (ref10 sliding-window double-scalar multiply +
+    one decompression + the final inversion), and one decompression
+    (ge_frombytes_negate_vartime, the per-kernel split's DECODE_OPS) is 19 M +
+    255 S, plus the conditional sqrt(-1) multiplication."""
+    import ctypes
+    import bench
+    lib = oracle.lib
+    lib.oracle_op_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.oracle_decode_op_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.oracle_decode_op_counts.restype = ctypes.c_int
+    rng = np.random.default_rng(5)
+    m, s = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    muls, sqs, dec = [], [], set()
+    for _ in range(64):
+        pk, sk = oracle.keypair(rng.bytes(32))
+        msg = rng.bytes(32)
+        assert oracle.verify(oracle.sign(msg, sk), msg, pk)
+        lib.oracle_op_counts(ctypes.byref(m), ctypes.byref(s))
+        muls.append(m.value)
+        sqs.append(s.value)
+        assert lib.oracle_decode_op_counts(pk, ctypes.byref(m), ctypes.byref(s)) == 0
+        dec.add((m.value, s.value))
+    assert abs(np.mean(muls) - 1520) < 0.02 * 1520 and abs(np.mean(sqs) - 1525) < 0.02 * 1525
+    assert dec <= {(19, 255), (20, 255)} and (19, 255) in dec
+    assert bench.DECODE_OPS == 64 * 19 + 36 * 255
+    assert bench.W_PREP + bench.W_MAIN == bench.W_VERIFY == 64 * 1520 + 36 * 1525 + 5520
