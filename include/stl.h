@@ -438,6 +438,11 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
                                         per device whose context (verify workspace ~0.44 GB, hash
                                         queue, checkSign scratch) libstl keeps; the least recently
                                         used one beyond it is freed */
+#define STL_TUNE_LONG_HASH 8        /* 0..62 (default 8; 0 off): in calls of at most two lane-pair chunks
+                                        (65,536 rows on 256 CUs), up to 1,024 of the longest preimages
+                                        of more than this many SHA-512 blocks are hashed one per wave
+                                        (schedules expanded side by side, rounds reading them from
+                                        LDS): the longest row sets a small ledger's hash latency */
 #define STL_TUNE_RCCL_TIMEOUT_MS 7 /* 1..3,600,000 (default 120,000; env STL_RCCL_TIMEOUT_S): deadline of
                                       stl_comm_init_rank and stl_comm_sync */
 int stl_debug_tuning(int key, int value);

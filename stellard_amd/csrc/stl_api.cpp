@@ -277,6 +277,7 @@ std::atomic<int> g_tune_streams{2};   // concurrent streams per device-resident 
 std::atomic<int> g_tune_sub_log2{0};  // log2 signatures per stream chunk; 0 = by batch size (chunk_for)
 std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
 std::atomic<int> g_tune_quad{3};      // smallest chunks' main kernel on lane groups: bit 0 quads, bit 1 duos
+std::atomic<int> g_tune_long_hash{8}; // small batches: rows of more than this many blocks hashed one per wave (0 off)
 
 // Chunk size of a device-resident call of n signatures over several streams
 // (DESIGN.md section 4): round(n / 2^18) chunks, at least two, of equal size
@@ -683,6 +684,14 @@ int ctx_queue(StreamCtx& c, size_t n, uint32_t** qws) {
 // tx-hash grid: 8 workgroups per CU (the kernel pulls preimages from a counter)
 uint32_t hash_grid(const Device& d) { return (uint32_t)d.cus * 8u; }
 
+// The hash kernel's long mode for a call of n preimages (DESIGN.md section 4,
+// small batches): on for calls of at most two lane-pair chunks -- latency-
+// bound, the chip mostly idle, the longest row's chain the hash's length --
+// off for throughput batches, where a wave per row would waste 63 lanes.
+uint32_t hash_long_min(const Device& d, size_t n) {
+  return n <= 2 * (size_t)pair_max(d) ? (uint32_t)g_tune_long_hash.load() : 0u;
+}
+
 uint32_t grid_for(const Device& d, size_t n) {
   const size_t tiles = (n + stl::kBlock - 1) / stl::kBlock;
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(tiles, d.grid));
@@ -907,7 +916,8 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
       STL_RC(copy_rows(s, dpre, b.bytes + base, c0, c1, &mark));
     STL_RC(s.join(d.copy, ks));
     if (b.mode == Mode::kPre)
-      STL_TRY(stl::launch_tx_hash(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, kctr, hash_grid(d), ks));
+      STL_TRY(stl::launch_tx_hash(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, kctr, hash_grid(d), ks,
+                                  hash_long_min(d, n)));
     else if (b.mode == Mode::kBlob)
       STL_TRY(stl::launch_tx_blob(dpre, doff + c0, dlen + c0, (uint32_t)cn, dmsg + 32 * c0, dsig + 64 * c0,
                                   dpk + 32 * c0, dtxid ? dtxid + 32 * c0 : nullptr, dstatus + c0, kctr,
@@ -1269,6 +1279,7 @@ int stl_debug_tuning(int key, int value) {
       case STL_TUNE_QUAD: return g_tune_quad.load();
       case STL_TUNE_STREAM_WORKSPACES: return g_max_caller_streams.load();
       case STL_TUNE_RCCL_TIMEOUT_MS: return g_rccl_timeout_ms.load();
+      case STL_TUNE_LONG_HASH: return g_tune_long_hash.load();
       default: return STL_EINVAL;
     }
   }
@@ -1297,6 +1308,9 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_RCCL_TIMEOUT_MS:
       if (value < 1 || value > 3600000) return STL_EINVAL;
       return g_rccl_timeout_ms.exchange(value);
+    case STL_TUNE_LONG_HASH:
+      if (value < 0 || value > 62) return STL_EINVAL;
+      return g_tune_long_hash.exchange(value);
     default:
       return STL_EINVAL;
   }
@@ -1662,7 +1676,8 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
       e = stl::launch_tx_blob(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, sig + 64 * b0, pk + 32 * b0,
                               id ? id + 32 * b0 : nullptr, st + b0, qw, hash_grid(d), js, kind);
     else
-      e = stl::launch_tx_hash(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, qw, hash_grid(d), js);
+      e = stl::launch_tx_hash(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, qw, hash_grid(d), js,
+                              hash_long_min(d, n));
     return e == hipSuccess ? STL_OK : STL_EHIP;
   };
   if (S == 1) {
@@ -1767,7 +1782,8 @@ int stl_tx_hash_batch_device(const uint8_t* d_preimages, const uint64_t* d_offse
   std::lock_guard<std::mutex> lk(c->mu);
   uint32_t* ctr = nullptr;
   STL_RC(ctx_queue(*c, n, &ctr));
-  STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(*d), s));
+  STL_TRY(stl::launch_tx_hash(d_preimages, d_offset, d_len, (uint32_t)n, d_msg, ctr, hash_grid(*d), s,
+                              hash_long_min(*d, n)));
   return STL_OK;
 }
 

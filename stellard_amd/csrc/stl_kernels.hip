@@ -1248,8 +1248,20 @@ __global__ __launch_bounds__(kBlock) void order_count_kernel(const uint32_t* __r
   if (threadIdx.x < kOrderBuckets && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 
-// exclusive scan of the 64 bucket counts into bucket cursors (one wave)
-__global__ __launch_bounds__(64) void order_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor) {
+// Rows hashed one per wave (tx_hash_kernel's long mode): at most this many,
+// the longest of the batch, and only rows of more than long_min blocks --
+// one long wave per SIMD of a 256-CU chip: two per SIMD run each block
+// ≈1.45x slower (8,000-row ledgers' hash 0.44 ms at 2,048 rows, profiles/r05/g).
+constexpr uint32_t kLongMaxRows = 1024;
+constexpr uint32_t kLongBatch = (64u * kWinBytes) / (80u * 8u);  // block schedules in a wave's window area
+
+// exclusive scan of the 64 bucket counts into bucket cursors (one wave); with
+// long_min > 0 also the number K of rows at the front of the order that the
+// hash kernel takes wave-wise -- min(kLongMaxRows, rows of more than
+// long_min blocks) -- in header[2], and header[0], the per-lane queue's
+// counter, starts after them
+__global__ __launch_bounds__(64) void order_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor,
+                                                        uint32_t* __restrict__ header, uint32_t long_min) {
   const uint32_t t = threadIdx.x;
   uint32_t v = hist[t];
 #pragma unroll
@@ -1258,6 +1270,12 @@ __global__ __launch_bounds__(64) void order_scan_kernel(const uint32_t* __restri
     if (t >= (uint32_t)d) v += u;
   }
   cursor[t] = v - hist[t];
+  // bucket t holds rows of 63 - t blocks (bucket 0: 63 or more), longest first
+  if (long_min > 0 && long_min < kOrderBuckets - 1u && t == kOrderBuckets - 2u - long_min) {
+    const uint32_t k = v < kLongMaxRows ? v : kLongMaxRows;
+    header[0] = k;
+    header[2] = k;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void order_scatter_kernel(const uint32_t* __restrict__ len, uint32_t n,
@@ -1281,6 +1299,78 @@ __global__ __launch_bounds__(kBlock) void order_scatter_kernel(const uint32_t* _
   }
 }
 
+// tx_hash_kernel's long mode (small batches: the longest row sets the
+// call's latency): the first K = counter[2] rows of the order, one per wave.
+// Lanes 0..kLongBatch-1 each load one block of the row (a 144-byte window of
+// 16-byte loads, as wave_window_fill takes them) and expand its schedule into
+// the wave's window area; the wave then runs the rounds block after block
+// reading W[t] from LDS (a broadcast read), so the schedule leaves the
+// dependent chain.
+__device__ __forceinline__ void hash_long_rows(const uint8_t* __restrict__ pre, const uint64_t* __restrict__ off,
+                                               const uint32_t* __restrict__ len, uint8_t* __restrict__ msg,
+                                               uint32_t* __restrict__ counter, const uint32_t* __restrict__ order,
+                                               uint4* win, uint32_t lane) {
+  uint2* wsch = reinterpret_cast<uint2*>(win);
+  // rows r = wave, wave + waves, ... < K: a static deal (the rows are the
+  // longest of the batch, about equal), every index a scalar, so the row loop
+  // is uniform control flow
+  const uint32_t K = __builtin_amdgcn_readfirstlane(counter[2]);
+  const uint32_t waves = gridDim.x * (kBlock / 64u);
+  const uint32_t first = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6));
+  for (uint32_t r = first; r < K; r += waves) {
+    const uint32_t row = order[r];
+    const uint8_t* p = pre + off[row];
+    const uint32_t L = len[row];
+    const uint32_t mis = (uint32_t)((uintptr_t)p & 3u);
+    const uintptr_t q = (uintptr_t)p - mis;  // aligned dword 0 of the message
+    const uintptr_t lo = (uintptr_t)p, end = lo + L;
+    const uint32_t nbl = (L + 17u + 127u) >> 7;
+    uint64_t st[8];
+    sha512_init(st);
+    for (uint32_t b0 = 0; b0 < nbl; b0 += kLongBatch) {
+      const uint32_t cnt = nbl - b0 < kLongBatch ? nbl - b0 : kLongBatch;
+      if (lane < cnt) {
+        const uint32_t blk = b0 + lane;
+        const uintptr_t blk_addr = q + 128u * blk;
+        const uintptr_t wbase = blk_addr & ~(uintptr_t)15;
+        uint32_t wr[4 * kWinChunks];
+#pragma unroll
+        for (uint32_t c = 0; c < kWinChunks; ++c) {
+          const uintptr_t a = wbase + 16u * c;
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (a < end && a + 16u > lo) v = *reinterpret_cast<const uint4*>(a);
+          wr[4 * c] = v.x; wr[4 * c + 1] = v.y; wr[4 * c + 2] = v.z; wr[4 * c + 3] = v.w;
+        }
+        uint64_t w[16];
+        block_from_window(w, wr, (uint32_t)(blk_addr & 15u) >> 2, mis, (int32_t)L - (int32_t)(128u * blk),
+                          blk + 1 == nbl, L, false, false, 0u);
+        uint2* dst = wsch + 80u * lane;
+        sha512_schedule(w, [&](int t, W64 v) { dst[t] = make_uint2(v.lo, v.hi); });
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint2* src = wsch + 80u * j;
+        sha512_rounds<true>(st, [&](int t) {
+          const uint2 v = src[t];
+          return W64{v.x, v.y};
+        });
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (lane == 0) {
+      uint32_t h[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+        h[2 * j + 1] = bswap32((uint32_t)st[j]);
+      }
+      st8(msg + 32 * (size_t)row, h);
+    }
+  }
+}
+
 // msg_i = SHA512Half(preimage_i) (Serializer.cpp:354-360 via
 // STObject::getSigningHash, SerializedObject.cpp:444-450).  Lanes pull
 // preimages from a global counter and advance one 128-byte block per
@@ -1294,6 +1384,8 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_hash_kerne
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
+  // Long mode (small batches): the first K rows of the order, one per wave
+  if (counter[2] != 0) hash_long_rows(pre, off, len, msg, counter, order, win, lane);
   ByteStream bs;
   bs.init(pre, 0);
   uint64_t st[8];
@@ -1748,7 +1840,8 @@ hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t*
 
 // queue workspace: [0] counter, [64..127] bucket counts, [128..191] cursors,
 // [256..) the order (n words)
-static hipError_t launch_order(const uint32_t* len, uint32_t n, uint32_t extra, uint32_t* qws, hipStream_t stream) {
+static hipError_t launch_order(const uint32_t* len, uint32_t n, uint32_t extra, uint32_t* qws, hipStream_t stream,
+                               uint32_t long_min = 0) {
   hipError_t e = hipMemsetAsync(qws, 0, kQueueHeaderBytes, stream);
   if (e != hipSuccess) return e;
   uint32_t* hist = qws + 64;
@@ -1757,19 +1850,24 @@ static hipError_t launch_order(const uint32_t* len, uint32_t n, uint32_t extra, 
   const uint32_t tiles = (n + kBlock - 1) / kBlock;
   const uint32_t grid = tiles < 1024u ? tiles : 1024u;
   hipLaunchKernelGGL(order_count_kernel, dim3(grid), dim3(kBlock), 0, stream, len, n, extra, hist);
-  hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(64), 0, stream, hist, cursor);
+  hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(64), 0, stream, hist, cursor, qws, long_min);
   hipLaunchKernelGGL(order_scatter_kernel, dim3(grid), dim3(kBlock), 0, stream, len, n, extra, cursor, order);
   return hipGetLastError();
 }
 
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          uint32_t* qws, uint32_t grid, hipStream_t stream) {
+                          uint32_t* qws, uint32_t grid, hipStream_t stream, uint32_t long_min) {
   if (n == 0) return hipSuccess;
-  hipError_t e = launch_order(len, n, 0u, qws, stream);
+  hipError_t e = launch_order(len, n, 0u, qws, stream, long_min);
   if (e != hipSuccess) return e;
-  const uint32_t blocks = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(tx_hash_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, pre, off, len, n,
-                     msg, qws, qws + kQueueHeaderBytes / 4);
+  uint32_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > grid) blocks = grid;
+  // long mode: waves 0..K-1 take the long rows first, so the grid gets
+  // kLongMaxRows waves on top of the per-lane queue's, which start on it at
+  // once (those the long rows do not need skip to the queue)
+  if (long_min) blocks += kLongMaxRows / (kBlock / 64u);
+  hipLaunchKernelGGL(tx_hash_kernel, dim3(blocks), dim3(kBlock), 0, stream, pre, off, len, n, msg, qws,
+                     qws + kQueueHeaderBytes / 4);
   return hipGetLastError();
 }
 

@@ -163,6 +163,69 @@ STL_HD void sha512_compress(uint64_t st[8], uint64_t w64in[16]) {
   st[6] = u64(add(w64(st[6]), g)); st[7] = u64(add(w64(st[7]), h));
 }
 
+// ---- compression over a precomputed message schedule ----
+// The latency path of a small batch (the longest preimage of a ledger: up to
+// 33 dependent compressions) hashes one long message per wave: the lanes
+// expand the schedules of up to kLongBatch blocks side by side (one lane per
+// block), and the rounds then read W[t] from LDS -- a third of a
+// compression's instructions leave its dependent chain.
+
+// W[16..79] of one block from w[0..15], each word handed to put(t, W[t]) as it
+// is made (a 16-word ring in registers).
+template <typename Put>
+STL_HD void sha512_schedule(const uint64_t win[16], Put put) {
+  W64 w[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    w[j] = w64(win[j]);
+    put(j, w[j]);
+  }
+#pragma unroll
+  for (int i = 16; i < 80; ++i) {
+    const W64 w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+    const W64 s0 = xor3(rotr<1>(w15), rotr<8>(w15), shr<7>(w15));
+    const W64 s1 = xor3(rotr<19>(w2), rotr<61>(w2), shr<6>(w2));
+    w[i & 15] = add(add(w[i & 15], s0), add(w[(i - 7) & 15], s1));
+    put(i, w[i & 15]);
+  }
+}
+
+// 64-bit add as one 64-bit VALU op (v_lshl_add_u64 on gfx950): no carry
+// through an SGPR, so no hazard nop -- the lone-wave latency path's add
+STL_HD W64 add64(W64 a, W64 b) { return w64(u64(a) + u64(b)); }
+
+// 80 rounds + feed-forward with W[t] = get(t), read kAhead rounds ahead of
+// their use (a ring in registers): the reads are pinned behind round
+// t - kAhead's state so the compiler neither hoists all 80 (160 VGPRs) nor
+// leaves a read's latency inside the chain.
+template <bool ADD64 = false, typename Get>
+STL_HD void sha512_rounds(uint64_t st[8], const Get& get) {
+  constexpr int kAhead = 8;
+  auto ad = [](W64 x, W64 y) { return ADD64 ? add64(x, y) : add(x, y); };
+  W64 a = w64(st[0]), b = w64(st[1]), c = w64(st[2]), d = w64(st[3]);
+  W64 e = w64(st[4]), f = w64(st[5]), g = w64(st[6]), h = w64(st[7]);
+  W64 ring[kAhead];
+#pragma unroll
+  for (int i = 0; i < kAhead; ++i) ring[i] = get(i);
+#pragma clang loop unroll(full)
+  for (int i = 0; i < 80; ++i) {
+    const W64 wi = ring[i % kAhead];
+    if (i + kAhead < 80) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      asm volatile("" : "+v"(a.lo), "+v"(e.lo)::"memory");
+#endif
+      ring[i % kAhead] = get(i + kAhead);
+    }
+    const W64 S1 = xor3(rotr<14>(e), rotr<18>(e), rotr<41>(e));
+    const W64 t1 = ad(ad(h, S1), ad(ad(ch(e, f, g), sha_kw(i)), wi));
+    const W64 S0 = xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a));
+    const W64 t2 = ad(S0, maj(a, b, c));
+    h = g; g = f; f = e; e = ad(d, t1); d = c; c = b; b = a; a = ad(t1, t2);
+  }
+  st[0] += u64(a); st[1] += u64(b); st[2] += u64(c); st[3] += u64(d);
+  st[4] += u64(e); st[5] += u64(f); st[6] += u64(g); st[7] += u64(h);
+}
+
 STL_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }

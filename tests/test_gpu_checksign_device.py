@@ -232,3 +232,74 @@ def test_blob_ledger_digests(stl, torch_cuda, blob_ledger):
     b = np.concatenate(bits)
     assert hashlib.sha256(np.packbits(b, bitorder="little").tobytes()).hexdigest() == want["bitmap_sha256"]
     assert sha(np.concatenate(sts)) == want["status_sha256"]
+
+
+@pytest.mark.timeout(300)
+def test_hash_long_mode_equals_hashlib(stl, torch_cuda):
+    """The hash kernel's long mode (STL_TUNE_LONG_HASH: small calls hash their
+    longest preimages one per wave, schedules expanded side by side and read
+    from LDS) gives SHA512Half exactly: against hashlib and the per-lane mode,
+    over unaligned offsets, every length from 1 to 12 KB around the block
+    edges, rows past one schedule batch (14 blocks) and past the 1,024-row cap,
+    and through the one-call checkSign (bits equal with the mode off)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(0x10C6)
+    edges = [128 * k + d for k in range(8, 96) for d in (-18, -17, -16, 0, 1, 111)]
+    lens = np.concatenate([np.arange(1, 300), np.array(edges), rng.integers(1, 12000, 3000)]).astype(np.int64)
+    lens = lens[lens > 0]
+    n = lens.size
+    gaps = rng.integers(0, 7, n)  # unaligned starts
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum(lens[:-1] + gaps[:-1])
+    buf = rng.integers(0, 256, int(offs[-1] + lens[-1] + 16), dtype=np.uint8)
+    want = np.array([np.frombuffer(hashlib.sha512(buf[o:o + ln].tobytes()).digest()[:32], np.uint8)
+                     for o, ln in zip(offs, lens)])
+    d_buf = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(offs).cuda()
+    d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+    old = stl.debug_tuning(stl.TUNE_LONG_HASH, -1)
+    try:
+        for lm in (8, 1, 0, 20):
+            stl.debug_tuning(stl.TUNE_LONG_HASH, lm)
+            got = stl.tx_hash_batch_device(d_buf, d_off, d_len).cpu().numpy()
+            assert np.array_equal(got, want), (lm, np.nonzero((got != want).any(1))[0][:10])
+        # more long rows than the cap: 3,000 rows of 10-40 blocks
+        big = rng.integers(1300, 5200, 3000).astype(np.int64)
+        boff = np.zeros(big.size, np.int64)
+        boff[1:] = np.cumsum(big[:-1])
+        bbuf = rng.integers(0, 256, int(boff[-1] + big[-1] + 16), dtype=np.uint8)
+        bwant = np.array([np.frombuffer(hashlib.sha512(bbuf[o:o + ln].tobytes()).digest()[:32], np.uint8)
+                          for o, ln in zip(boff, big)])
+        stl.debug_tuning(stl.TUNE_LONG_HASH, 8)
+        got = stl.tx_hash_batch_device(torch.from_numpy(bbuf).cuda(), torch.from_numpy(boff).cuda(),
+                                       torch.from_numpy(big.astype(np.int32)).cuda()).cpu().numpy()
+        assert np.array_equal(got, bwant)
+    finally:
+        stl.debug_tuning(stl.TUNE_LONG_HASH, old)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.timeout(300)
+def test_checksign_long_mode_same_bits(stl, torch_cuda, ledger):
+    """Small one-call checkSign calls (the small-ledger latency path) give the
+    same bits with the long hash mode on and off, over ledger slices of 1 to
+    60,000 rows."""
+    torch = torch_cuda
+    lp, d_pre, d_off, d_len, sig, pk = ledger
+    old = stl.debug_tuning(stl.TUNE_LONG_HASH, -1)
+    try:
+        for lo, m in ((0, 1), (64, 1000), (4096, 3837), (1 << 18, 19001), (700_032, 60_000)):
+            sl = slice(lo, lo + m)
+            bits = []
+            for lm in (0, 8):
+                stl.debug_tuning(stl.TUNE_LONG_HASH, lm)
+                w = stl.tx_verify_batch_device(d_pre, d_off[sl], d_len[sl], sig[sl], pk[sl])
+                torch.cuda.synchronize()
+                bits.append(stl.words_to_bool(w, m))
+            assert np.array_equal(bits[0], bits[1]), (lo, m)
+            expect = np.ones(m, bool)
+            bad = lp["bad"][(lp["bad"] >= lo) & (lp["bad"] < lo + m)] - lo
+            expect[bad] = False
+            assert np.array_equal(bits[1], expect), (lo, m)
+    finally:
+        stl.debug_tuning(stl.TUNE_LONG_HASH, old)

@@ -25,6 +25,8 @@ def main():
     V.init()
     if os.environ.get("PROBE_QUAD"):  # A/B of the quad main kernel (STL_TUNE_QUAD)
         V.debug_tuning(V.TUNE_QUAD, int(os.environ["PROBE_QUAD"]))
+    if os.environ.get("PROBE_LONG"):  # A/B of the hash kernel's long mode (STL_TUNE_LONG_HASH)
+        V.debug_tuning(V.TUNE_LONG_HASH, int(os.environ["PROBE_LONG"]))
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream()
     lp = datasets.ledger_plan()
