@@ -675,8 +675,8 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
 // Hash work queue of stream context c for n rows (counter + longest-first
 // order, stl::hash_queue_bytes(n)).  Caller holds c.mu until the hash kernel
 // using it is enqueued (a concurrent grow would free it first -- ADVICE r4).
-int ctx_queue(StreamCtx& c, size_t n, uint32_t** qws) {
-  STL_RC(c.queue.ensure(stl::hash_queue_bytes(n)));
+int ctx_queue(StreamCtx& c, size_t n, uint32_t** qws, bool blob = false) {
+  STL_RC(c.queue.ensure(blob ? stl::blob_queue_bytes(n) : stl::hash_queue_bytes(n)));
   *qws = static_cast<uint32_t*>(c.queue.p);
   return STL_OK;
 }
@@ -871,7 +871,9 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
     STL_RC(d.pre.ensure(bytes + 16));
     STL_RC(d.off.ensure(n * 8));
     STL_RC(d.len.ensure(n * 4));
-    STL_RC(d.ctr.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
+    const size_t qn = std::min(n, kPipeChunk);
+    const size_t qbytes = b.mode == Mode::kBlob ? stl::blob_queue_bytes(qn) : stl::hash_queue_bytes(qn);
+    STL_RC(d.ctr.ensure(qbytes));
     if (b.mode == Mode::kBlob) {
       STL_RC(d.status.ensure(n));
       if (b.txid) STL_RC(d.txid.ensure(n * 32));
@@ -900,7 +902,10 @@ int enqueue_shard(const Batch& b, Shard& s, size_t words_alloc) {
       std::lock_guard<std::mutex> lk(c->mu);
       STL_RC(c->ws.ensure(stl::verify_ws_bytes(d.grid, true)));
     }
-  if (two && b.mode != Mode::kSig) STL_RC(d.ctr2.ensure(stl::hash_queue_bytes(std::min(n, kPipeChunk))));
+  if (two && b.mode != Mode::kSig) {
+    const size_t qn = std::min(n, kPipeChunk);
+    STL_RC(d.ctr2.ensure(b.mode == Mode::kBlob ? stl::blob_queue_bytes(qn) : stl::hash_queue_bytes(qn)));
+  }
   for (size_t c0 = 0; c0 < n; c0 += kPipeChunk) {
     const size_t c1 = std::min(n, c0 + kPipeChunk), cn = c1 - c0;
     const bool odd = two && ((c0 / kPipeChunk) & 1);
@@ -1639,8 +1644,8 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   // the hash queues under the locks held through the launches below: pool
   // stream 1's context is shared by every caller stream
   uint32_t* q[2] = {nullptr, nullptr};
-  STL_RC(ctx_queue(*kc[0], S > 1 ? sub : n, &q[0]));
-  if (S > 1) STL_RC(ctx_queue(*kc[1], n - sub, &q[1]));
+  STL_RC(ctx_queue(*kc[0], S > 1 ? sub : n, &q[0], blob));
+  if (S > 1) STL_RC(ctx_queue(*kc[1], n - sub, &q[1], blob));
   const size_t row = blob ? 128 : 32;
   STL_RC(c.scratch.ensure(std::max<size_t>(n, 1) * row));
   uint8_t* msg = static_cast<uint8_t*>(c.scratch.p);
@@ -1800,7 +1805,7 @@ int stl_signed_blob_prepare_device(uint32_t kind, const uint8_t* d_blobs, const 
   const std::shared_ptr<StreamCtx> c = stream_ctx(*d, s);
   std::lock_guard<std::mutex> lk(c->mu);
   uint32_t* ctr = nullptr;
-  STL_RC(ctx_queue(*c, n, &ctr));
+  STL_RC(ctx_queue(*c, n, &ctr, true));
   STL_TRY(stl::launch_tx_blob(d_blobs, d_offset, d_len, (uint32_t)n, d_msg, d_sig, d_pk, d_id, d_status, ctr,
                               hash_grid(*d), s, kind));
   return STL_OK;

@@ -120,10 +120,15 @@ hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t*
 // cursors of the longest-first order) and the order itself.
 constexpr size_t kQueueHeaderBytes = 1024;
 inline size_t hash_queue_bytes(size_t n) { return kQueueHeaderBytes + 4 * n; }
+// The blob path's queue also holds each row's layout from the parse kernel
+// (32 B: status and the cut ranges), 16-byte aligned after the order.
+inline size_t blob_layout_offset(size_t n) { return (hash_queue_bytes(n) + 15) / 16 * 16; }
+inline size_t blob_queue_bytes(size_t n) { return blob_layout_offset(n) + 32 * n; }
 // long_min > 0: up to 1,024 of the longest rows of more than long_min SHA-512
 // blocks are hashed one per wave (the latency path of small batches)
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint32_t* qws, uint32_t grid, hipStream_t stream, uint32_t long_min = 0);
+// qws: blob_queue_bytes(n)
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
                           hipStream_t stream, uint32_t kind = 0u /* STL_BLOB_* */);

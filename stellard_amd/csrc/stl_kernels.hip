@@ -1436,6 +1436,59 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_hash_kerne
   }
 }
 
+// The canonical-form pass of every blob (stl_txblob.h tx_blob_parse), one
+// lane per row, ahead of the hashing (the blob ledger ran 10 %
+// behind preimages): the field walk is a chain of dependent byte loads, which
+// inside the hash kernel stalled a whole wave at every refill; here many
+// small waves hide it.  Writes each row's status, the verify inputs a row
+// gets from its bytes (signature and key; the always-reject signature, a
+// zero key and message for a deferred or malformed row; a zero id for a
+// deferred one) and the row's layout for the hash kernel: {status, xs0, xe0,
+// xs1}, {xe1, xs2, xe2, 0}.
+__global__ __launch_bounds__(kBlock) void tx_blob_parse_kernel(const uint8_t* __restrict__ blobs,
+                                                               const uint64_t* __restrict__ off,
+                                                               const uint32_t* __restrict__ len, uint32_t n,
+                                                               uint8_t* __restrict__ msg, uint8_t* __restrict__ sig,
+                                                               uint8_t* __restrict__ pk, uint8_t* __restrict__ txid,
+                                                               uint8_t* __restrict__ status, uint4* __restrict__ layout,
+                                                               BlobKind kind) {
+  for (uint32_t mi = blockIdx.x * kBlock + threadIdx.x; mi < n; mi += gridDim.x * kBlock) {
+    const uint8_t* b = blobs + off[mi];
+    const uint32_t L = len[mi];
+    TxLayout t;
+    tx_blob_parse(b, L, t, kind.sig_code, kind.min_len, kind.format);
+    // an STL_TX_OK row has one cut, its signature field (every other
+    // non-signing field is outside both templates); the hash kernel's splice
+    // relies on it, so anything else is deferred (never taken)
+    if (t.status == kTxOk && t.xs1 != L) t.status = kTxDeferred;
+    status[mi] = (uint8_t)t.status;
+    layout[2 * (size_t)mi] = make_uint4(t.status, t.xs0, t.xe0, t.xs1);
+    layout[2 * (size_t)mi + 1] = make_uint4(t.xe1, t.xs2, t.xe2, 0u);
+    uint4* sq = reinterpret_cast<uint4*>(sig + 64 * (size_t)mi);
+    if (t.status == kTxOk) {
+      uint32_t sgw[16], pkw[8];
+      blob_words(sgw, b, t.sig_off, 16, L);
+      blob_words(pkw, b, t.pk_off, 8, L);
+      sq[0] = make_uint4(sgw[0], sgw[1], sgw[2], sgw[3]);
+      sq[1] = make_uint4(sgw[4], sgw[5], sgw[6], sgw[7]);
+      sq[2] = make_uint4(sgw[8], sgw[9], sgw[10], sgw[11]);
+      sq[3] = make_uint4(sgw[12], sgw[13], sgw[14], sgw[15]);
+      st8(pk + 32 * (size_t)mi, pkw);
+    } else {
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u), f = make_uint4(~0u, ~0u, ~0u, ~0u);
+      sq[0] = z; sq[1] = z; sq[2] = f; sq[3] = f;
+      uint4* pq = reinterpret_cast<uint4*>(pk + 32 * (size_t)mi);
+      pq[0] = z; pq[1] = z;
+      uint4* mq = reinterpret_cast<uint4*>(msg + 32 * (size_t)mi);
+      mq[0] = z; mq[1] = z;
+      if (t.status == kTxDeferred && txid != nullptr) {
+        uint4* tq = reinterpret_cast<uint4*>(txid + 32 * (size_t)mi);
+        tq[0] = z; tq[1] = z;
+      }
+    }
+  }
+}
+
 // Serialized transactions -> verify inputs.  Same work queue as
 // tx_hash_kernel; a lane runs the canonical-form pass when it takes a blob,
 // then one SHA-512 block per iteration: first the signing hash
@@ -1448,14 +1501,18 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
                                                          uint8_t* __restrict__ msg, uint8_t* __restrict__ sig,
                                                          uint8_t* __restrict__ pk, uint8_t* __restrict__ txid,
                                                          uint8_t* __restrict__ status, uint32_t* __restrict__ counter,
-                                                         const uint32_t* __restrict__ order, BlobKind kind) {
+                                                         const uint32_t* __restrict__ order,
+                                                         const uint4* __restrict__ layout, BlobKind kind) {
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
-  SpliceStream ss;  // phase 0: sign prefix || blob minus the cut fields
-  ByteStream bs;    // phase 1: [the 4 bytes before the blob, word 0 -> id prefix] || blob
-  ss.init(blobs, 0, kind.sign_prefix, nullptr);
+  // phase 0: sign prefix || blob[0, cxs) || blob[cxe, len) -- an STL_TX_OK row
+  // has exactly one cut, its signature field (splice1_block); phase 1:
+  // [the 4 bytes before the blob, word 0 -> id prefix] || blob
+  ByteStream bs;
   bs.init(blobs, 0);
+  uint32_t cxs = 0, cxe = 0;
+  const uint32_t sign_le = bswap32(kind.sign_prefix);
   const uint32_t txn_le = bswap32(kind.id_prefix);
   const bool id_pfx = kind.id_prefixed != 0;
   const uint32_t pfx_bytes = id_pfx ? 4u : 0u;
@@ -1480,39 +1537,23 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
           b = blobs + off[mi];
           const uint32_t L = len[mi];
           bend = b + L;
-          TxLayout t;
-          tx_blob_parse(b, L, t, kind.sig_code, kind.min_len, kind.format);
-          status[mi] = (uint8_t)t.status;
-          uint4* sq = reinterpret_cast<uint4*>(sig + 64 * (size_t)mi);
-          if (t.status == kTxOk) {
-            uint32_t sgw[16], pkw[8];
-            blob_words(sgw, b, t.sig_off, 16, L);
-            blob_words(pkw, b, t.pk_off, 8, L);
-            sq[0] = make_uint4(sgw[0], sgw[1], sgw[2], sgw[3]);
-            sq[1] = make_uint4(sgw[4], sgw[5], sgw[6], sgw[7]);
-            sq[2] = make_uint4(sgw[8], sgw[9], sgw[10], sgw[11]);
-            sq[3] = make_uint4(sgw[12], sgw[13], sgw[14], sgw[15]);
-            st8(pk + 32 * (size_t)mi, pkw);
-            ss.init(b, L, kind.sign_prefix, &t);
-            nb = ss.blocks();
+          // the row's layout from tx_blob_parse_kernel (status, sig, pk, the
+          // reject inputs and a deferred row's zero id are written there)
+          const uint4 la = layout[2 * (size_t)mi], lb = layout[2 * (size_t)mi + 1];
+          const uint32_t row_status = la.x;
+          (void)lb;  // the second and third cuts: none on an STL_TX_OK row
+          if (row_status == kTxOk) {
+            cxs = la.y;
+            cxe = la.z;
+            nb = (4u + L - (cxe - cxs) + 17u + 127u) >> 7;
             phase = 0;
           } else {
-            const uint4 z = make_uint4(0u, 0u, 0u, 0u), f = make_uint4(~0u, ~0u, ~0u, ~0u);
-            sq[0] = z; sq[1] = z; sq[2] = f; sq[3] = f;
-            uint4* pq = reinterpret_cast<uint4*>(pk + 32 * (size_t)mi);
-            pq[0] = z; pq[1] = z;
-            uint4* mq = reinterpret_cast<uint4*>(msg + 32 * (size_t)mi);
-            mq[0] = z; mq[1] = z;
             bs.init(b - pfx_bytes, L + pfx_bytes);
             nb = bs.blocks();
             phase = 1;
           }
-          if (t.status == kTxDeferred || (phase == 1 && txid == nullptr)) {
-            if (txid != nullptr) {
-              uint4* tq = reinterpret_cast<uint4*>(txid + 32 * (size_t)mi);
-              tq[0] = make_uint4(0u, 0u, 0u, 0u);
-              tq[1] = make_uint4(0u, 0u, 0u, 0u);
-            }
+          if (row_status == kTxDeferred || (phase == 1 && txid == nullptr)) {
+            // nothing to hash (the parse kernel wrote everything)
           } else {
             blk = 0;
             sha512_init(st);
@@ -1523,7 +1564,12 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
     }
     if (!__any(active)) break;
     const uintptr_t blk_addr = (uintptr_t)(bs.q + 32 * blk);
-    const uintptr_t wsrc = phase == 0 ? (uintptr_t)ss.cursor() : blk_addr;
+    // phase 0: the window starts at the blob byte of the block's first
+    // preimage word -- past the cut once the block starts after it; a block
+    // that holds the cut reads its later words with global loads (WinSrc)
+    const uint32_t p0 = 128u * blk;
+    const uintptr_t splice_src = (uintptr_t)b + p0 - 4u + (p0 >= 4u + cxs ? cxe - cxs : 0u);
+    const uintptr_t wsrc = phase == 0 ? splice_src : blk_addr;
     const uintptr_t wbase = active ? (wsrc & ~(uintptr_t)15) : 0;
     wave_window_fill(win, wbase, (uintptr_t)b, (uintptr_t)bend, lane);
     if (active) {
@@ -1531,7 +1577,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
       uint64_t w[16];
       if (phase == 0) {
         const WinSrc src{lw, wbase, nullptr};
-        ss.block(w, blk, blk + 1 == nb, src);
+        splice1_block(w, b, (uint32_t)(bend - b), cxs, cxe, sign_le, blk, blk + 1 == nb, src);
       } else {
         block_from_window(w, lw, (uint32_t)(blk_addr & 15u) >> 2, bs.mis, (int32_t)bs.len - (int32_t)(128 * blk),
                           blk + 1 == nb, bs.len, blk == 0, id_pfx, txn_le);
@@ -1876,11 +1922,16 @@ hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint3
                           hipStream_t stream, uint32_t kind_id) {
   if (n == 0) return hipSuccess;
   const BlobKind kind = kind_id == 1u ? blob_kind_validation() : blob_kind_tx();
+  uint4* layout = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qws) + blob_layout_offset(n));
+  const uint32_t blocks = (n + kBlock - 1) / kBlock;
+  // parse: one lane per row, up to 16 workgroups per CU's worth of grid
+  const uint32_t pgrid = 2u * grid;
+  hipLaunchKernelGGL(tx_blob_parse_kernel, dim3(blocks < pgrid ? blocks : pgrid), dim3(kBlock), 0, stream, blobs, off,
+                     len, n, msg, sig, pk, txid, status, layout, kind);
   hipError_t e = launch_order(len, n, kind.id_prefixed ? 4u : 0u, qws, stream);
   if (e != hipSuccess) return e;
-  const uint32_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(tx_blob_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, blobs, off, len,
-                     n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4, kind);
+                     n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4, layout, kind);
   return hipGetLastError();
 }
 

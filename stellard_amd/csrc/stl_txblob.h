@@ -515,6 +515,59 @@ struct SpliceStream {
   STL_HD const uint8_t* end() const { return b + len; }
 };
 
+// Block blk of a one-cut signing preimage, prefix || blob[0, xs) ||
+// blob[xe, len) -- every STL_TX_OK transaction or validation has exactly one
+// cut, its signature field -- as 16 big-endian words with the FIPS 180-4
+// padding, assembled word by word: a preimage word at byte P comes from the
+// blob at P - 4 (before the cut) or P - 4 + (xe - xs) (after it), one
+// unaligned dword each (two aligned dwords and a v_alignbyte), the word that
+// straddles the cut from both.  src(q) returns the aligned blob dword at q
+// (the kernel's LDS window, global loads outside it); dwords wholly outside
+// the blob are never asked for.  Same words as SpliceStream, without its byte
+// funnel (tests/test_txblob.py compares the two on random layouts).
+template <typename Src>
+STL_HD void splice1_block(uint64_t w[16], const uint8_t* b, uint32_t len, uint32_t xs, uint32_t xe,
+                          uint32_t prefix_le, uint32_t blk, bool last, const Src& src) {
+  const uint32_t cut = xe - xs, total = 4u + len - cut, pb = 4u + xs;
+  const uintptr_t lo = (uintptr_t)b, hi = lo + len;
+  auto dw = [&](uintptr_t q) -> uint32_t {  // aligned dword q, 0 outside the blob
+    return (q + 4u <= lo || q >= hi) ? 0u : src(reinterpret_cast<const uint8_t*>(q));
+  };
+  auto udw = [&](uintptr_t a) -> uint32_t {  // dword at byte address a (any alignment)
+    const uintptr_t q = a & ~(uintptr_t)3;
+    return align_byte(dw(q + 4u), dw(q), (uint32_t)(a & 3u));
+  };
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t m[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t P = 128u * blk + 4u * (uint32_t)(2 * j + h);
+      uint32_t v;
+      if (P == 0) {
+        v = prefix_le;
+      } else {
+        const int32_t k = (int32_t)pb - (int32_t)P;  // bytes of this word before the cut
+        v = udw(lo + P - 4u + (k > 0 ? 0u : cut));
+        if (k > 0 && k < 4) {
+          const uint32_t mk = (1u << (8 * k)) - 1u;
+          v = (v & mk) | (udw(lo + P - 4u + cut) & ~mk);
+        }
+      }
+      const int32_t r = (int32_t)total - (int32_t)P;  // preimage bytes from this word on
+      const int32_t rc = r < 0 ? 0 : (r > 4 ? 4 : r);
+      const uint32_t keep = rc == 4 ? 0xffffffffu : ((1u << (8 * rc)) - 1u);
+      const uint32_t pad = (r >= 0 && r < 4) ? (0x80u << (8 * rc)) : 0u;
+      m[h] = (v & keep) | pad;
+    }
+    w[j] = be64_from_le32(m[0], m[1]);
+  }
+  if (last) {
+    w[14] = 0;
+    w[15] = (uint64_t)total * 8u;
+  }
+}
+
 // n little-endian words from blob bytes [off, off + 4n) (off unaligned).
 STL_HD void blob_words(uint32_t* out, const uint8_t* b, uint32_t off, uint32_t n, uint32_t len) {
   const uint32_t sh = (uint32_t)((uintptr_t)(b + off) & 3u);
@@ -529,6 +582,25 @@ STL_HD void blob_words(uint32_t* out, const uint8_t* b, uint32_t off, uint32_t n
     for (uint32_t i = 0; i < n; ++i)
       out[i] = (uint32_t)b[off + 4 * i] | ((uint32_t)b[off + 4 * i + 1] << 8) |
                ((uint32_t)b[off + 4 * i + 2] << 16) | ((uint32_t)b[off + 4 * i + 3] << 24);
+  }
+}
+
+// SHA512Half of a one-cut preimage through splice1_block (host tests).
+STL_HD void splice1_sha512_half(uint32_t out[8], const uint8_t* blob, uint32_t len, uint32_t prefix, uint32_t xs,
+                                uint32_t xe) {
+  const uint32_t total = 4u + len - (xe - xs), nb = (total + 17u + 127u) / 128u;
+  uint64_t st[8], w[16];
+  sha512_init(st);
+  const uint32_t prefix_le = bswap32(prefix);
+  for (uint32_t k = 0; k < nb; ++k) {
+    splice1_block(w, blob, len, xs, xe, prefix_le, k, k + 1 == nb,
+                  [](const uint8_t* q) { return *reinterpret_cast<const uint32_t*>(q); });
+    sha512_compress(st, w);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+    out[2 * j + 1] = bswap32((uint32_t)st[j]);
   }
 }
 

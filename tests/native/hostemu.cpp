@@ -452,4 +452,18 @@ int hostemu_tx_format(uint32_t type, uint64_t* allowed, uint64_t* required) {
 uint64_t hostemu_declared_names(uint32_t type) { return stl::declared_names(type); }
 int hostemu_validation_field(uint32_t code) { return stl::validation_field(code) ? 1 : 0; }
 int hostemu_non_signing_field(uint32_t code) { return stl::non_signing_field(code) ? 1 : 0; }
+
+// SpliceStream and splice1_block over the same one-cut layout (the two
+// preimage assemblies of tx_blob_kernel): SHA512Half of each
+void hostemu_splice_pair(const uint8_t* blob, uint32_t len, uint32_t prefix, uint32_t xs, uint32_t xe,
+                         uint8_t out_stream[32], uint8_t out_words[32]) {
+  stl::TxLayout t;
+  t.xs0 = xs; t.xe0 = xe;
+  t.xs1 = t.xe1 = t.xs2 = t.xe2 = len;
+  uint32_t a[8], b[8];
+  stl::splice_sha512_half(a, blob, len, prefix, &t);
+  stl::splice1_sha512_half(b, blob, len, prefix, xs, xe);
+  std::memcpy(out_stream, a, 32);
+  std::memcpy(out_words, b, 32);
+}
 }

@@ -322,3 +322,35 @@ def test_blob_ledger_construction(oracle, emu):
         expect[list(kinds[k])] = False
     assert np.array_equal(bits, expect)
     assert 100 <= min(bp["lens"]) and max(bp["lens"]) <= 4100
+
+
+def test_splice_word_assembly_equals_stream(emu):
+    """tx_blob_kernel's word-wise one-cut splice (stl_txblob.h splice1_block)
+    against SpliceStream and hashlib: SHA512Half(prefix || blob[0, xs) ||
+    blob[xe, len)) over random lengths, cut positions and buffer alignments,
+    including cuts at the blob's edges and preimages ending in every byte of a
+    block."""
+    import ctypes
+    from tests.oracle_bind import _buf
+    emu.hostemu_splice_pair.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(0x5911CE)
+    cases = [(L, xs, xe) for L in (32, 66, 67, 100, 127, 128, 129, 200) for xs in (0, 1, 3, 5) for xe in (xs, xs + 66)
+             if xe <= L]
+    for _ in range(3000):
+        L = int(rng.integers(32, 5000))
+        xs = int(rng.integers(0, L))
+        xe = int(rng.integers(xs, min(L, xs + 300) + 1))
+        cases.append((L, xs, xe))
+    for L in range(160, 420):  # every preimage length across two block edges
+        cases.append((L, 80, 146))
+    a, w = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+    for i, (L, xs, xe) in enumerate(cases):
+        sh = i % 16
+        arr = np.zeros(L + 64, np.uint8)
+        arr[sh:sh + L] = rng.integers(0, 256, L, dtype=np.uint8)
+        blob = arr[sh:sh + L].tobytes()
+        ptr = ctypes.c_void_p(arr.ctypes.data + sh)
+        emu.hostemu_splice_pair(ptr, L, 0x53545800, xs, xe, a, w)
+        want = hashlib.sha512(b"STX\x00" + blob[:xs] + blob[xe:]).digest()[:32]
+        assert a.raw == want and w.raw == want, (L, xs, xe, sh)
