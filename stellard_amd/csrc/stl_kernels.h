@@ -121,9 +121,12 @@ hipError_t launch_hram_var(const uint8_t* sig, const uint8_t* pk, const uint8_t*
 constexpr size_t kQueueHeaderBytes = 1024;
 inline size_t hash_queue_bytes(size_t n) { return kQueueHeaderBytes + 4 * n; }
 // The blob path's queue also holds each row's layout from the parse kernel
-// (32 B: status and the cut ranges), 16-byte aligned after the order.
+// (32 B: status and the cut ranges), 16-byte aligned after the order, and
+// each row's spliced block (128 B: the SHA-512 block of the signing preimage
+// that holds the cut, assembled by the parse kernel).
 inline size_t blob_layout_offset(size_t n) { return (hash_queue_bytes(n) + 15) / 16 * 16; }
-inline size_t blob_queue_bytes(size_t n) { return blob_layout_offset(n) + 32 * n; }
+inline size_t blob_side_offset(size_t n) { return blob_layout_offset(n) + 32 * n; }
+inline size_t blob_queue_bytes(size_t n) { return blob_side_offset(n) + 128 * n; }
 // long_min > 0: up to 1,024 of the longest rows of more than long_min SHA-512
 // blocks are hashed one per wave (the latency path of small batches)
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,

@@ -1438,42 +1438,124 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_hash_kerne
 
 // The canonical-form pass of every blob (stl_txblob.h tx_blob_parse), one
 // lane per row, ahead of the hashing (the blob ledger ran 10 %
-// behind preimages): the field walk is a chain of dependent byte loads, which
-// inside the hash kernel stalled a whole wave at every refill; here many
-// small waves hide it.  Writes each row's status, the verify inputs a row
-// gets from its bytes (signature and key; the always-reject signature, a
-// zero key and message for a deferred or malformed row; a zero id for a
-// deferred one) and the row's layout for the hash kernel: {status, xs0, xe0,
-// xs1}, {xe1, xs2, xe2, 0}.
-__global__ __launch_bounds__(kBlock) void tx_blob_parse_kernel(const uint8_t* __restrict__ blobs,
+// behind preimages).  A lane-per-row walk over global memory makes every load
+// instruction touch 64 cache lines, one per row, so the wave first stages the
+// first kParseStage bytes of its 64 rows in LDS with 16-byte loads dealt
+// across the lanes (12 instructions, about a dozen lines each); the walk, the
+// signature and key and the spliced block then read LDS (a Payment's fields
+// up to its memos lie inside; the rest are global loads).  Writes each row's
+// status and layout {status, xs, xe, 0} -- an STL_TX_OK row has exactly one
+// cut, its signature field (every other non-signing field is outside both
+// templates), so a row with more is deferred (never taken) -- the verify
+// inputs (signature and key; the always-reject signature, a zero key and
+// message for a deferred or malformed row; a zero id for a deferred one) and,
+// for an STL_TX_OK row, the SHA-512 block of its signing preimage that holds
+// the cut (splice1_words): the hash kernel reads every block as a plain
+// window.
+#ifndef STL_PARSE_STAGE
+#define STL_PARSE_STAGE 192
+#endif
+constexpr uint32_t kParseStage = STL_PARSE_STAGE;
+constexpr uint32_t kParseChunks = kParseStage / 16u;
+constexpr uint32_t kParseStride = kParseStage / 4u + 1u;  // dwords per row, odd: no bank conflicts
+static_assert(kParseChunks * 16u == kParseStage && kParseChunks <= 64u, "stage: whole 16-byte chunks");
+
+struct StagedBytes {  // b[i] of a blob whose first bytes are staged in LDS
+  const uint8_t* g;
+  const uint8_t* s;  // LDS copy of the aligned 16-byte granules from g - off
+  uint32_t off;
+  __device__ uint8_t operator[](uint32_t i) const {
+    const uint32_t j = i + off;
+    return j < kParseStage ? s[j] : g[i];
+  }
+};
+
+struct StagedDwords {  // aligned blob dwords: LDS inside the stage, global outside
+  const uint32_t* s;
+  uintptr_t base;
+  __device__ uint32_t operator()(const uint8_t* q) const {
+    const uintptr_t o = (uintptr_t)q - base;
+    return o < kParseStage ? s[o >> 2] : *reinterpret_cast<const uint32_t*>(q);
+  }
+};
+
+// n little-endian words from blob bytes [pos, pos + 4n): LDS when inside the
+// stage (sh = the blob's offset in its first granule), else blob_words
+__device__ __forceinline__ void staged_words(uint32_t* out, const uint32_t* s, uint32_t sh, const uint8_t* b,
+                                             uint32_t pos, uint32_t n, uint32_t len) {
+  const uint32_t j = sh + pos;
+  if (j + 4u * n + 4u <= kParseStage) {
+    const uint32_t q = j >> 2, r = j & 3u;
+    for (uint32_t i = 0; i < n; ++i) out[i] = align_byte(s[q + i + 1], s[q + i], r);
+  } else {
+    blob_words(out, b, pos, n, len);
+  }
+}
+
+__global__ __launch_bounds__(kBlock, 3) void tx_blob_parse_kernel(const uint8_t* __restrict__ blobs,
                                                                const uint64_t* __restrict__ off,
                                                                const uint32_t* __restrict__ len, uint32_t n,
                                                                uint8_t* __restrict__ msg, uint8_t* __restrict__ sig,
                                                                uint8_t* __restrict__ pk, uint8_t* __restrict__ txid,
                                                                uint8_t* __restrict__ status, uint4* __restrict__ layout,
-                                                               BlobKind kind) {
-  for (uint32_t mi = blockIdx.x * kBlock + threadIdx.x; mi < n; mi += gridDim.x * kBlock) {
-    const uint8_t* b = blobs + off[mi];
-    const uint32_t L = len[mi];
+                                                               uint4* __restrict__ side, BlobKind kind) {
+  __shared__ uint32_t stage_all[kBlock * kParseStride];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t* wstage = stage_all + (threadIdx.x & ~63u) * kParseStride;  // the wave's 64 rows
+  uint32_t* stage = stage_all + threadIdx.x * kParseStride;           // this lane's row
+  const uint32_t sign_le = bswap32(kind.sign_prefix);
+  // tiles of kBlock rows: every lane of a wave takes part in every staging
+  for (uint32_t tile = blockIdx.x * kBlock; tile < n; tile += gridDim.x * kBlock) {
+    const uint32_t mi = tile + threadIdx.x;
+    const bool valid = mi < n;
+    const uint8_t* b = blobs;
+    uint32_t L = 0;
+    if (valid) {
+      b = blobs + off[mi];
+      L = len[mi];
+    }
+    const uintptr_t lo = (uintptr_t)b, end = lo + L, base = lo & ~(uintptr_t)15;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (uint32_t k = 0; k < kParseChunks; ++k) {
+      const uint32_t g = k * 64u + lane, r = g / kParseChunks, c = g - r * kParseChunks;
+      const uintptr_t rb = (uintptr_t)shfl_u64(base, r), re = (uintptr_t)shfl_u64(end, r);
+      const uintptr_t a = rb + 16u * c;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (a < re) v = *reinterpret_cast<const uint4*>(a);
+      uint32_t* d = wstage + r * kParseStride + 4u * c;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (!valid) continue;
+    const uint32_t sh = (uint32_t)(lo - base);
+    const StagedBytes sb{b, reinterpret_cast<const uint8_t*>(stage), sh};
     TxLayout t;
-    tx_blob_parse(b, L, t, kind.sig_code, kind.min_len, kind.format);
-    // an STL_TX_OK row has one cut, its signature field (every other
-    // non-signing field is outside both templates); the hash kernel's splice
-    // relies on it, so anything else is deferred (never taken)
+    tx_blob_parse(sb, L, t, kind.sig_code, kind.min_len, kind.format);
     if (t.status == kTxOk && t.xs1 != L) t.status = kTxDeferred;
     status[mi] = (uint8_t)t.status;
-    layout[2 * (size_t)mi] = make_uint4(t.status, t.xs0, t.xe0, t.xs1);
-    layout[2 * (size_t)mi + 1] = make_uint4(t.xe1, t.xs2, t.xe2, 0u);
+    layout[2 * (size_t)mi] = make_uint4(t.status, t.xs0, t.xe0, 0u);
     uint4* sq = reinterpret_cast<uint4*>(sig + 64 * (size_t)mi);
     if (t.status == kTxOk) {
       uint32_t sgw[16], pkw[8];
-      blob_words(sgw, b, t.sig_off, 16, L);
-      blob_words(pkw, b, t.pk_off, 8, L);
+      staged_words(sgw, stage, sh, b, t.sig_off, 16, L);
+      staged_words(pkw, stage, sh, b, t.pk_off, 8, L);
       sq[0] = make_uint4(sgw[0], sgw[1], sgw[2], sgw[3]);
       sq[1] = make_uint4(sgw[4], sgw[5], sgw[6], sgw[7]);
       sq[2] = make_uint4(sgw[8], sgw[9], sgw[10], sgw[11]);
       sq[3] = make_uint4(sgw[12], sgw[13], sgw[14], sgw[15]);
       st8(pk + 32 * (size_t)mi, pkw);
+      // the preimage block holding the cut (preimage byte 4 + xs0)
+      uint32_t m[32];
+      splice1_words(m, b, L, t.xs0, t.xe0, sign_le, (4u + t.xs0) >> 7, StagedDwords{stage, base});
+      uint4* dq = side + 8 * (size_t)mi;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dq[j] = make_uint4(m[4 * j], m[4 * j + 1], m[4 * j + 2], m[4 * j + 3]);
     } else {
       const uint4 z = make_uint4(0u, 0u, 0u, 0u), f = make_uint4(~0u, ~0u, ~0u, ~0u);
       sq[0] = z; sq[1] = z; sq[2] = f; sq[3] = f;
@@ -1502,16 +1584,19 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
                                                          uint8_t* __restrict__ pk, uint8_t* __restrict__ txid,
                                                          uint8_t* __restrict__ status, uint32_t* __restrict__ counter,
                                                          const uint32_t* __restrict__ order,
-                                                         const uint4* __restrict__ layout, BlobKind kind) {
+                                                         const uint4* __restrict__ layout,
+                                                         const uint4* __restrict__ side, BlobKind kind) {
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
   // phase 0: sign prefix || blob[0, cxs) || blob[cxe, len) -- an STL_TX_OK row
-  // has exactly one cut, its signature field (splice1_block); phase 1:
-  // [the 4 bytes before the blob, word 0 -> id prefix] || blob
+  // has exactly one cut, its signature field: blocks before block sb read the
+  // blob 4 bytes early (word 0 -> sign prefix), block sb is the parse
+  // kernel's spliced block, blocks after it read the blob past the cut;
+  // phase 1: [the 4 bytes before the blob, word 0 -> id prefix] || blob
   ByteStream bs;
   bs.init(blobs, 0);
-  uint32_t cxs = 0, cxe = 0;
+  uint32_t cxs = 0, cut = 0, sblk = 0, total = 0;
   const uint32_t sign_le = bswap32(kind.sign_prefix);
   const uint32_t txn_le = bswap32(kind.id_prefix);
   const bool id_pfx = kind.id_prefixed != 0;
@@ -1539,13 +1624,14 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
           bend = b + L;
           // the row's layout from tx_blob_parse_kernel (status, sig, pk, the
           // reject inputs and a deferred row's zero id are written there)
-          const uint4 la = layout[2 * (size_t)mi], lb = layout[2 * (size_t)mi + 1];
+          const uint4 la = layout[2 * (size_t)mi];
           const uint32_t row_status = la.x;
-          (void)lb;  // the second and third cuts: none on an STL_TX_OK row
           if (row_status == kTxOk) {
             cxs = la.y;
-            cxe = la.z;
-            nb = (4u + L - (cxe - cxs) + 17u + 127u) >> 7;
+            cut = la.z - la.y;
+            sblk = (4u + cxs) >> 7;
+            total = 4u + L - cut;
+            nb = (total + 17u + 127u) >> 7;
             phase = 0;
           } else {
             bs.init(b - pfx_bytes, L + pfx_bytes);
@@ -1563,25 +1649,29 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
       }
     }
     if (!__any(active)) break;
-    const uintptr_t blk_addr = (uintptr_t)(bs.q + 32 * blk);
-    // phase 0: the window starts at the blob byte of the block's first
-    // preimage word -- past the cut once the block starts after it; a block
-    // that holds the cut reads its later words with global loads (WinSrc)
     const uint32_t p0 = 128u * blk;
-    const uintptr_t splice_src = (uintptr_t)b + p0 - 4u + (p0 >= 4u + cxs ? cxe - cxs : 0u);
-    const uintptr_t wsrc = phase == 0 ? splice_src : blk_addr;
+    const bool spliced = phase == 0 && blk == sblk;
+    // window source: the block's first message byte (phase 0: of the blob,
+    // 4 bytes early, past the cut after block sblk; the spliced block's slot)
+    uintptr_t wsrc = (uintptr_t)(bs.q + 32 * blk), wlo = (uintptr_t)b, wend = (uintptr_t)bend;
+    uint32_t mis = bs.mis, tot = bs.len;
+    if (phase == 0) {
+      wsrc = (uintptr_t)b + p0 - 4u + (blk > sblk ? cut : 0u);
+      tot = total;
+      if (spliced) {
+        wsrc = (uintptr_t)(side + 8 * (size_t)mi);
+        wlo = wsrc;
+        wend = wsrc + 128u;
+      }
+      mis = (uint32_t)(wsrc & 3u);
+    }
     const uintptr_t wbase = active ? (wsrc & ~(uintptr_t)15) : 0;
-    wave_window_fill(win, wbase, (uintptr_t)b, (uintptr_t)bend, lane);
+    wave_window_fill(win, wbase, wlo, wend, lane);
     if (active) {
       const uint32_t* lw = reinterpret_cast<const uint32_t*>(win) + lane * (kWinBytes / 4);
       uint64_t w[16];
-      if (phase == 0) {
-        const WinSrc src{lw, wbase, nullptr};
-        splice1_block(w, b, (uint32_t)(bend - b), cxs, cxe, sign_le, blk, blk + 1 == nb, src);
-      } else {
-        block_from_window(w, lw, (uint32_t)(blk_addr & 15u) >> 2, bs.mis, (int32_t)bs.len - (int32_t)(128 * blk),
-                          blk + 1 == nb, bs.len, blk == 0, id_pfx, txn_le);
-      }
+      block_from_window(w, lw, (uint32_t)(wsrc & 15u) >> 2, mis, (int32_t)tot - (int32_t)p0, blk + 1 == nb, tot,
+                        blk == 0 && !spliced, phase == 1 ? id_pfx : true, phase == 1 ? txn_le : sign_le);
       sha512_compress(st, w);
       if (++blk == nb) {
         uint32_t h[8];
@@ -1923,15 +2013,16 @@ hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint3
   if (n == 0) return hipSuccess;
   const BlobKind kind = kind_id == 1u ? blob_kind_validation() : blob_kind_tx();
   uint4* layout = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qws) + blob_layout_offset(n));
+  uint4* side = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qws) + blob_side_offset(n));
   const uint32_t blocks = (n + kBlock - 1) / kBlock;
-  // parse: one lane per row, up to 16 workgroups per CU's worth of grid
+  // parse: one lane per row, two rounds of the chip's resident workgroups
   const uint32_t pgrid = 2u * grid;
   hipLaunchKernelGGL(tx_blob_parse_kernel, dim3(blocks < pgrid ? blocks : pgrid), dim3(kBlock), 0, stream, blobs, off,
-                     len, n, msg, sig, pk, txid, status, layout, kind);
+                     len, n, msg, sig, pk, txid, status, layout, side, kind);
   hipError_t e = launch_order(len, n, kind.id_prefixed ? 4u : 0u, qws, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tx_blob_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, blobs, off, len,
-                     n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4, layout, kind);
+                     n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4, layout, side, kind);
   return hipGetLastError();
 }
 

@@ -254,15 +254,18 @@ struct TxLayout {
   uint32_t xs0, xe0, xs1, xe1, xs2, xe2;
 };
 
-STL_HD bool bytes_nonzero(const uint8_t* b, uint32_t pos, uint32_t n) {
+template <typename Bytes>
+STL_HD bool bytes_nonzero(const Bytes& b, uint32_t pos, uint32_t n) {
   uint32_t acc = 0;
   for (uint32_t i = 0; i < n; ++i) acc |= b[pos + i];
   return acc != 0;
 }
 
-// The canonical-form pass over one blob (one lane).  Byte loads only: fields
-// are short and the pass is a few percent of the hashing that follows.
-STL_HD void tx_blob_parse(const uint8_t* b, uint32_t len, TxLayout& t, uint32_t sig_code = kCodeTxnSignature,
+// The canonical-form pass over one blob (one lane).  Byte reads only, b[i]
+// for i < len: a plain pointer, or the device's staged reader (the blob's
+// first bytes in LDS, tx_blob_parse_kernel).
+template <typename Bytes>
+STL_HD void tx_blob_parse(const Bytes& b, uint32_t len, TxLayout& t, uint32_t sig_code = kCodeTxnSignature,
                           uint32_t min_len = kTxMinBytes, uint32_t format = kFormatTx) {
   t.status = kTxDeferred;
   t.pk_off = t.sig_off = 0;
@@ -526,8 +529,8 @@ struct SpliceStream {
 // the blob are never asked for.  Same words as SpliceStream, without its byte
 // funnel (tests/test_txblob.py compares the two on random layouts).
 template <typename Src>
-STL_HD void splice1_block(uint64_t w[16], const uint8_t* b, uint32_t len, uint32_t xs, uint32_t xe,
-                          uint32_t prefix_le, uint32_t blk, bool last, const Src& src) {
+STL_HD void splice1_words(uint32_t m[32], const uint8_t* b, uint32_t len, uint32_t xs, uint32_t xe,
+                          uint32_t prefix_le, uint32_t blk, const Src& src) {
   const uint32_t cut = xe - xs, total = 4u + len - cut, pb = 4u + xs;
   const uintptr_t lo = (uintptr_t)b, hi = lo + len;
   auto dw = [&](uintptr_t q) -> uint32_t {  // aligned dword q, 0 outside the blob
@@ -538,11 +541,9 @@ STL_HD void splice1_block(uint64_t w[16], const uint8_t* b, uint32_t len, uint32
     return align_byte(dw(q + 4u), dw(q), (uint32_t)(a & 3u));
   };
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    uint32_t m[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t P = 128u * blk + 4u * (uint32_t)(2 * j + h);
+  for (int i = 0; i < 32; ++i) {
+    {
+      const uint32_t P = 128u * blk + 4u * (uint32_t)i;
       uint32_t v;
       if (P == 0) {
         v = prefix_le;
@@ -558,13 +559,22 @@ STL_HD void splice1_block(uint64_t w[16], const uint8_t* b, uint32_t len, uint32
       const int32_t rc = r < 0 ? 0 : (r > 4 ? 4 : r);
       const uint32_t keep = rc == 4 ? 0xffffffffu : ((1u << (8 * rc)) - 1u);
       const uint32_t pad = (r >= 0 && r < 4) ? (0x80u << (8 * rc)) : 0u;
-      m[h] = (v & keep) | pad;
+      m[i] = (v & keep) | pad;
     }
-    w[j] = be64_from_le32(m[0], m[1]);
   }
+}
+
+// The same block as 16 big-endian words, with the length in the final block.
+template <typename Src>
+STL_HD void splice1_block(uint64_t w[16], const uint8_t* b, uint32_t len, uint32_t xs, uint32_t xe,
+                          uint32_t prefix_le, uint32_t blk, bool last, const Src& src) {
+  uint32_t m[32];
+  splice1_words(m, b, len, xs, xe, prefix_le, blk, src);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = be64_from_le32(m[2 * j], m[2 * j + 1]);
   if (last) {
     w[14] = 0;
-    w[15] = (uint64_t)total * 8u;
+    w[15] = (uint64_t)(4u + len - (xe - xs)) * 8u;
   }
 }
 

@@ -466,4 +466,47 @@ void hostemu_splice_pair(const uint8_t* blob, uint32_t len, uint32_t prefix, uin
   std::memcpy(out_stream, a, 32);
   std::memcpy(out_words, b, 32);
 }
+
+// tx_blob_kernel's phase 0 on the host: blocks before the cut's block read
+// the blob 4 bytes early, the cut's block is tx_blob_parse_kernel's spliced
+// block (splice1_words), later blocks read past the cut -- each through a
+// 144-byte window of 16-byte granules (zero outside [lo, end)), as
+// wave_window_fill and block_from_window take it.
+void hostemu_splice_kernel(const uint8_t* blob, uint32_t len, uint32_t prefix, uint32_t xs, uint32_t xe,
+                           uint8_t out[32]) {
+  const uint32_t cut = xe - xs, total = 4u + len - cut, nb = (total + 17u + 127u) / 128u, sblk = (4u + xs) >> 7;
+  const uint32_t prefix_le = stl::bswap32(prefix);
+  uint32_t side[32];
+  stl::splice1_words(side, blob, len, xs, xe, prefix_le, sblk,
+                     [](const uint8_t* q) { return *reinterpret_cast<const uint32_t*>(q); });
+  uint64_t st[8], w[16];
+  stl::sha512_init(st);
+  for (uint32_t blk = 0; blk < nb; ++blk) {
+    const bool spliced = blk == sblk;
+    uintptr_t src = (uintptr_t)blob + 128u * blk - 4u + (blk > sblk ? cut : 0u);
+    uintptr_t lo = (uintptr_t)blob, end = lo + len;
+    if (spliced) {
+      src = (uintptr_t)side;
+      lo = src;
+      end = src + 128u;
+    }
+    const uintptr_t base = src & ~(uintptr_t)15;
+    uint32_t win[36];
+    for (uint32_t c = 0; c < 9; ++c) {
+      const uintptr_t a = base + 16u * c;
+      for (int k = 0; k < 4; ++k)
+        win[4 * c + k] = (a < end && a + 16u > lo) ? reinterpret_cast<const uint32_t*>(a)[k] : 0u;
+    }
+    stl::block_from_window(w, win, (uint32_t)(src & 15u) >> 2, (uint32_t)(src & 3u),
+                           (int32_t)total - (int32_t)(128u * blk), blk + 1 == nb, total, blk == 0 && !spliced, true,
+                           prefix_le);
+    stl::sha512_compress(st, w);
+  }
+  uint32_t h[8];
+  for (int j = 0; j < 4; ++j) {
+    h[2 * j] = stl::bswap32((uint32_t)(st[j] >> 32));
+    h[2 * j + 1] = stl::bswap32((uint32_t)st[j]);
+  }
+  std::memcpy(out, h, 32);
+}
 }

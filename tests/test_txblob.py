@@ -325,8 +325,9 @@ def test_blob_ledger_construction(oracle, emu):
 
 
 def test_splice_word_assembly_equals_stream(emu):
-    """tx_blob_kernel's word-wise one-cut splice (stl_txblob.h splice1_block)
-    against SpliceStream and hashlib: SHA512Half(prefix || blob[0, xs) ||
+    """The word-wise one-cut splice (stl_txblob.h splice1_block) and
+    tx_blob_kernel's block schedule (the parse kernel's spliced block between
+    plain windows, hostemu_splice_kernel) against SpliceStream and hashlib: SHA512Half(prefix || blob[0, xs) ||
     blob[xe, len)) over random lengths, cut positions and buffer alignments,
     including cuts at the blob's edges and preimages ending in every byte of a
     block."""
@@ -344,7 +345,9 @@ def test_splice_word_assembly_equals_stream(emu):
         cases.append((L, xs, xe))
     for L in range(160, 420):  # every preimage length across two block edges
         cases.append((L, 80, 146))
-    a, w = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+    emu.hostemu_splice_kernel.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_void_p]
+    a, w, k = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
     for i, (L, xs, xe) in enumerate(cases):
         sh = i % 16
         arr = np.zeros(L + 64, np.uint8)
@@ -352,5 +355,6 @@ def test_splice_word_assembly_equals_stream(emu):
         blob = arr[sh:sh + L].tobytes()
         ptr = ctypes.c_void_p(arr.ctypes.data + sh)
         emu.hostemu_splice_pair(ptr, L, 0x53545800, xs, xe, a, w)
+        emu.hostemu_splice_kernel(ptr, L, 0x53545800, xs, xe, k)
         want = hashlib.sha512(b"STX\x00" + blob[:xs] + blob[xe:]).digest()[:32]
-        assert a.raw == want and w.raw == want, (L, xs, xe, sh)
+        assert a.raw == want and w.raw == want and k.raw == want, (L, xs, xe, sh)
