@@ -3,7 +3,9 @@
 config1_leg's construction) through stl_tx_blob_verify_batch, K timed calls;
 run under rocprofv3 --kernel-trace --memory-copy-trace to see where a call's
 time goes.  Prints the median ms and the per-call host times.
-    python3 tools/host_blob_probe.py [K] [n]"""
+    python3 tools/host_blob_probe.py [K] [n] [device]
+With `device`: the device-resident one call (stl_signed_blob_verify_batch_device)
+on blobs already in HBM instead."""
 import ctypes
 import json
 import os
@@ -39,6 +41,20 @@ def main():
     blobs = blobs_from_preimages(pre, tsig.cpu().numpy(), tpk.cpu().numpy())
     buf, offs, lens = pack(blobs)
     buf = np.concatenate([buf, np.zeros(4, np.uint8)])
+    if len(sys.argv) > 3 and sys.argv[3] == "device":
+        d_buf = torch.from_numpy(buf).cuda()
+        d_off = torch.from_numpy(offs.view(np.int64)).cuda()
+        d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+        words = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
+        ts = []
+        for _ in range(K + 1):
+            t0 = time.perf_counter()
+            V.signed_blob_verify_batch_device(d_buf, d_off, d_len, out_words=words)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        print(json.dumps({"n": n, "mode": "device", "ms_median": float(np.median(ts[1:])),
+                          "ms": [round(t, 3) for t in ts], "accepted": int(V.words_to_bool(words, n).sum())}))
+        return
     B = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     bm = np.zeros((n + 7) // 8, np.uint8)
     st = np.zeros(n, np.uint8)
