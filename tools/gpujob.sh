@@ -20,6 +20,12 @@
 #   py:SCRIPT[:ARGS]   python3 tools/SCRIPT ARGS (comma-separated ARGS), stdout to OUT/SCRIPT.log
 #   exec:N:K:R:SPECS   tools/exec_ab.py on N signatures, K launches x R rotations, settings
 #                      SPECS (name=fused,queue,streams,log2 separated by +), to OUT/exec_N.json
+#   abpy:SCRIPT:ARGS:V1,V2  ABBA of python3 tools/SCRIPT ARGS (comma-separated) over libstl
+#                      builds build/ab/V.so ("base" = the product), each run's last stdout
+#                      line appended to OUT/SCRIPT_V.jsonl (hash_bench.py, prep_probe.py,
+#                      host_blob_probe.py, small_batch_probe.py)
+#   trace:SCRIPT:ARGS  rocprofv3 --kernel-trace --memory-copy-trace of python3 tools/SCRIPT
+#                      ARGS, CSVs under OUT/trace_SCRIPT
 set -o pipefail
 OUT=$1; shift
 [ -n "$OUT" ] || { echo "usage: tools/gpujob.sh OUT STEP..."; exit 2; }
@@ -76,6 +82,22 @@ for step in "$@"; do
     py:*)
       IFS=: read -r _ S A <<< "$step"
       run ${S%.py} 600 python3 -u tools/$S ${A//,/ } || exit $? ;;
+    abpy:*)
+      IFS=: read -r _ S A VS <<< "$step"
+      IFS=, read -r -a vs <<< "$VS"
+      order=("${vs[@]}")
+      for ((i=${#vs[@]}-1; i>=0; i--)); do order+=("${vs[$i]}"); done
+      for v in "${order[@]}"; do
+        lib=""; [ "$v" != base ] && lib=build/ab/$v.so
+        STL_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/$S ${A//,/ } > $D/${S%.py}_$v.out 2>> $D/${S%.py}.err
+        rc=$?; echo "$S variant $v rc=$rc: $(tail -c 300 $D/${S%.py}_$v.out | tail -1)"
+        [ $rc -eq 0 ] || exit $rc
+        tail -1 $D/${S%.py}_$v.out >> $D/${S%.py}_$v.jsonl
+      done ;;
+    trace:*)
+      IFS=: read -r _ S A <<< "$step"
+      run trace_${S%.py} 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+        -d $D/trace_${S%.py} -o run -- python3 -u tools/$S ${A//,/ } || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
