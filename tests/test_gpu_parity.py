@@ -406,6 +406,59 @@ def test_tx_blob_special_cases_and_corpus(stl, oracle):
     assert (exp["status"] == 0).sum() > 400
 
 
+def test_tx_blob_cut_in_later_blocks(stl, oracle, torch_cuda):
+    """Payments whose TxnSignature starts past the first SHA-512 block of the
+    signing preimage (every optional field before it: tags, the last ledger
+    sequence, PreviousTxnID / AccountTxnID / InvoiceID, IOU Amount and SendMax
+    -- up to 4 + 270 bytes): the parse kernel assembles block 1 or 2 as the
+    spliced block and the hash kernel reads the blocks around it as plain
+    windows.  Bits, statuses and IDs equal the oracle's, through the host API
+    and the device-resident one call."""
+    torch = torch_cuda
+    from tests import txblob as T
+    from tests.oracle_bind import pack_blobs
+    rng = np.random.default_rng(0xC075)
+    ks = T.keys(oracle, 4, 0xC075)
+    cur = b"\0" * 12 + b"USD" + b"\0" * 5
+    blobs, xs = [], []
+    for i in range(600):
+        pk, sk = ks[i % 4]
+        fs = [T.Field(T.TransactionType, T.u16(0)), T.Field(T.Flags, T.u32(0x80000000)),
+              T.Field(T.Sequence, T.u32(i + 1)), T.Field(T.Fee, T.amount_native(10)),
+              T.Field(T.SigningPubKey, T.vl(pk)), T.Field(T.Account, T.vl(T.account_id(pk))),
+              T.Field(T.Destination, T.vl(rng.bytes(20)))]
+        if rng.random() < 0.8:
+            fs.append(T.Field(T.Amount, T.amount_iou(int(rng.integers(10**15, 10**16)), 0, cur, rng.bytes(20))))
+        else:
+            fs.append(T.Field(T.Amount, T.amount_native(int(rng.integers(1, 10**11)))))
+        opt = [(T.SourceTag, T.u32(int(rng.integers(0, 2**32)))), (T.DestinationTag, T.u32(7)),
+               (T.LastLedgerSequence, T.u32(99)), ((T.HASH256, 5), rng.bytes(32)),  # PreviousTxnID
+               (T.AccountTxnID, rng.bytes(32)), (T.InvoiceID, rng.bytes(32)),
+               (T.SendMax, T.amount_iou(int(rng.integers(10**15, 10**16)), 0, cur, rng.bytes(20)))]
+        for fid, v in opt:
+            if rng.random() < 0.85:
+                fs.append(T.Field(fid, v))
+        if rng.random() < 0.3:
+            fs.append(T.Field(T.Memos, T.array_value([(T.Memo, [T.Field(T.MemoData, T.vl(rng.bytes(int(rng.integers(0, 600)))))])])))
+        blob, _, sig = T.signed_blob(fs, sk, oracle.sign)
+        blobs.append(blob)
+        xs.append(blob.find(b"\x74\x40" + bytes(sig)))
+    xs = np.array(xs)
+    assert (xs >= 0).all() and ((4 + xs) // 128 >= 1).sum() > 300 and ((4 + xs) // 128 == 2).sum() > 50, \
+        np.bincount((4 + xs) // 128)
+    exp = _blob_expectations(oracle, blobs)
+    assert (exp["status"] == 0).all()
+    bits, st, ids = stl.tx_blob_verify_batch(blobs, tx_ids=True)
+    _check_blob_results(bits, st, ids, exp)
+    assert bits.all()
+    buf, offs, lens = pack_blobs(blobs)
+    out = stl.signed_blob_verify_batch_device(torch.from_numpy(buf).cuda(), torch.from_numpy(offs.astype(np.int64)).cuda(),
+                                              torch.from_numpy(lens.astype(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert stl.words_to_bool(out["words"], len(blobs)).all()
+    assert np.array_equal(out["status"].cpu().numpy(), st)
+
+
 def test_tx_blob_fuzz(stl, oracle):
     from tests import txblob as T
     base = T.valid_corpus(oracle, 200, seed=5)
