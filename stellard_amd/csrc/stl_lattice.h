@@ -252,6 +252,16 @@ STL_HD void lat_madd2(uint32_t out[5], uint32_t ua, const uint32_t A[5], uint32_
 // (X, Y) when  r >= M1 + q M2  and  y - r >= M1 + (q + 1) M2;  the step is
 // also taken only while the new remainder is certainly >= 2^128 (the exact
 // Euclid's stopping rule) and the matrix stays below 2^32.
+// At most kLehmerSteps certified steps per round: a wave runs each round's
+// loop to its slowest lane, and lanes certify 8-30 quotients from 53 bits
+// (tools/lattice_sim.cpp, 2,000 waves of random k: 121.6 iterations in 7.03
+// rounds per wave uncapped; 95.7 in 7.15 at 16, the rows unchanged -- every
+// step is still an exact Euclid step, only some move to the next round).
+#ifndef STL_LEHMER_STEPS
+#define STL_LEHMER_STEPS 16
+#endif
+constexpr int kLehmerSteps = STL_LEHMER_STEPS;
+
 STL_HD void lat_lehmer_round(uint32_t rl[8], uint32_t rs[8], uint32_t tl[5], uint32_t ts[5], bool& tl_neg, bool& ok,
                              bool act) {
   double x, y, thr;
@@ -259,7 +269,7 @@ STL_HD void lat_lehmer_round(uint32_t rl[8], uint32_t rs[8], uint32_t tl[5], uin
   double m00 = 1.0, m01 = 0.0, m10 = 0.0, m11 = 1.0;
   bool go = act, odd = false;
 #pragma unroll 1
-  for (int it = 0; it < 64; ++it) {
+  for (int it = 0; it < kLehmerSteps; ++it) {
     if (!lat_any(go)) break;
     double q = floor(lat_div_est(x, y));
     double r = fma(-q, y, x);
