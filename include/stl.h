@@ -73,7 +73,8 @@ extern "C" {
  * (stl_kernels.h kDedupBytes: hash slots, key arrays, decoded keys, shared and
  * wide key tables), allocated once per device for the host batch API and once
  * per (device, stream) -- per library stream too, and for at most
- * STL_TUNE_STREAM_WORKSPACES caller streams -- for the device-resident API; does not pay when keys are all distinct.  Chunks small enough for lane
+ * STL_TUNE_STREAM_WORKSPACES caller streams -- for the device-resident API.
+ * Does not pay when keys are all distinct.  Chunks small enough for lane
  * pairs or quads (STL_ONE_LANE below) run on them instead: latency-bound
  * there, the pairs and quads are faster. */
 #define STL_DEDUP_KEYS 0x8u
