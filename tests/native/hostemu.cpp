@@ -24,7 +24,12 @@ static void hostemu_check_subk(const stl::fe& a, const stl::fe& b, int k);
 #include "../../stellard_amd/csrc/stl_base_table.h"
 #include "../../stellard_amd/csrc/stl_txblob.h"
 #include "../../stellard_amd/csrc/stl_verify_core.h"
+// HOSTEMU_SANITIZE_SUBSET (tests/native/sanitize_main.cpp): only the product
+// verify path and the blob pass are compiled -- the sanitized build of every
+// table-layout variant and the signer took over twelve minutes
+#ifndef HOSTEMU_SANITIZE_SUBSET
 #include "../../stellard_amd/csrc/stl_sign.h"
+#endif
 
 static double alpha(const stl::fe& a) {
   uint32_t m = 0;
@@ -114,6 +119,7 @@ uint64_t hostemu_verify_batch_mode(const uint8_t* sig, const uint8_t* msg, const
   return g_bound_viol.load();
 }
 
+#ifndef HOSTEMU_SANITIZE_SUBSET
 // The product path (mode 0) with the kernels' split table layout
 // (TableView::split): heads of entries 1-8 in one array, entry 0's head one
 // shared identity line, tails in a separate array at stride `tstride` quads
@@ -236,6 +242,8 @@ uint64_t hostemu_verify_batch_pair(const uint8_t* sig, const uint8_t* msg, const
   }
   return g_bound_viol.load();
 }
+
+#endif  // HOSTEMU_SANITIZE_SUBSET
 
 // Words of the identity entry's head as the split tables expect it (the
 // device constant kIdentityHead must equal these 32 words).
@@ -416,6 +424,7 @@ void hostemu_fe_invert_bytes(const uint8_t a[32], uint8_t out[32]) {
   std::memcpy(out, wo, 32);
 }
 
+#ifndef HOSTEMU_SANITIZE_SUBSET
 // stl_sign.h on the host: the honest rows and the adversarial rows the GPU's
 // sign kernel builds (stl_debug_sign_adversarial_device), on 8 threads.
 void hostemu_sign_adversarial(const uint8_t* seed, const uint8_t* msg, const uint8_t* cls, const uint32_t* param,
@@ -440,6 +449,7 @@ void hostemu_sign_adversarial(const uint8_t* seed, const uint8_t* msg, const uin
     });
   for (auto& x : th) x.join();
 }
+#endif  // HOSTEMU_SANITIZE_SUBSET
 }
 
 // ---- the device pass's field tables (tests/test_sfields.py pins them to the

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <vector>
 
+#define HOSTEMU_SANITIZE_SUBSET  // the verify path and the blob pass only
 #include "hostemu.cpp"
 
 extern "C" {
