@@ -1345,13 +1345,18 @@ __device__ __forceinline__ void hash_long_rows(const uint8_t* __restrict__ pre, 
         block_from_window(w, wr, (uint32_t)(blk_addr & 15u) >> 2, mis, (int32_t)L - (int32_t)(128u * blk),
                           blk + 1 == nbl, L, false, false, 0u);
         uint2* dst = wsch + 80u * lane;
-        sha512_schedule(w, [&](int t, W64 v) { dst[t] = make_uint2(v.lo, v.hi); });
+        // W[t] + K[t]: the round constant added here, in parallel over the
+        // lanes, instead of on the wave's chain of rounds
+        sha512_schedule(w, [&](int t, W64 v) {
+          const W64 kw = add64(v, w64(sha_k(t)));
+          dst[t] = make_uint2(kw.lo, kw.hi);
+        });
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint2* src = wsch + 80u * j;
-        sha512_rounds<true>(st, [&](int t) {
+        sha512_rounds<true, true>(st, [&](int t) {
           const uint2 v = src[t];
           return W64{v.x, v.y};
         });

@@ -198,7 +198,9 @@ STL_HD W64 add64(W64 a, W64 b) { return w64(u64(a) + u64(b)); }
 // their use (a ring in registers): the reads are pinned behind round
 // t - kAhead's state so the compiler neither hoists all 80 (160 VGPRs) nor
 // leaves a read's latency inside the chain.
-template <bool ADD64 = false, typename Get>
+// With KW, get(t) returns W[t] + K[t] (the caller folded the round constant
+// into the schedule, off the rounds' chain).
+template <bool ADD64 = false, bool KW = false, typename Get>
 STL_HD void sha512_rounds(uint64_t st[8], const Get& get) {
   constexpr int kAhead = 8;
   auto ad = [](W64 x, W64 y) { return ADD64 ? add64(x, y) : add(x, y); };
@@ -217,7 +219,7 @@ STL_HD void sha512_rounds(uint64_t st[8], const Get& get) {
       ring[i % kAhead] = get(i + kAhead);
     }
     const W64 S1 = xor3(rotr<14>(e), rotr<18>(e), rotr<41>(e));
-    const W64 t1 = ad(ad(h, S1), ad(ad(ch(e, f, g), sha_kw(i)), wi));
+    const W64 t1 = KW ? ad(ad(h, S1), ad(ch(e, f, g), wi)) : ad(ad(h, S1), ad(ad(ch(e, f, g), sha_kw(i)), wi));
     const W64 S0 = xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a));
     const W64 t2 = ad(S0, maj(a, b, c));
     h = g; g = f; f = e; e = ad(d, t1); d = c; c = b; b = a; a = ad(t1, t2);

@@ -89,10 +89,11 @@ for step in "$@"; do
       for ((i=${#vs[@]}-1; i>=0; i--)); do order+=("${vs[$i]}"); done
       for v in "${order[@]}"; do
         lib=""; [ "$v" != base ] && lib=build/ab/$v.so
-        STL_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/$S ${A//,/ } > $D/${S%.py}_$v.out 2>> $D/${S%.py}.err
-        rc=$?; echo "$S variant $v rc=$rc: $(tail -c 300 $D/${S%.py}_$v.out | tail -1)"
+        STL_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/$S ${A//,/ } > $D/${S%.py}_run.out 2>> $D/${S%.py}.err
+        rc=$?; echo "$S variant $v rc=$rc: $(tail -c 300 $D/${S%.py}_run.out | tail -1)"
         [ $rc -eq 0 ] || exit $rc
-        tail -1 $D/${S%.py}_$v.out >> $D/${S%.py}_$v.jsonl
+        cat $D/${S%.py}_run.out >> $D/${S%.py}_$v.out
+        tail -1 $D/${S%.py}_run.out >> $D/${S%.py}_$v.jsonl
       done ;;
     trace:*)
       IFS=: read -r _ S A <<< "$step"
