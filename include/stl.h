@@ -296,11 +296,15 @@ void stl_comm_destroy(void);
  * waiting for peers) -- the teardown after a failed or timed-out gather. */
 void stl_comm_abort(void);
 /* hipStreamSynchronize(stream) with the RCCL deadline (timeout_ms, or the
- * library's when <= 0): while the stream has not drained, the communicator's
- * asynchronous error is polled; an RCCL error or the deadline aborts the
- * communicator (which ends a stalled gather's kernels) and returns
- * STL_ERCCL, so a rank whose peers never arrive can fall back instead of
- * hanging. */
+ * library's when <= 0) on the gather: the work queued on the stream ahead of
+ * the last stl_bitmap_gather(v)_device is waited for first (a lapse of 10x the
+ * deadline, or of the library's deadline if longer, there is STL_EHIP and
+ * keeps the communicator), then, while the
+ * stream has not drained, the communicator's asynchronous error is polled; an
+ * RCCL error or the deadline aborts the communicator (which ends a stalled
+ * gather's kernels) and returns STL_ERCCL, so a rank whose peers never arrive
+ * can fall back instead of hanging.  A gather whose enqueue fails or times
+ * out aborts the communicator the same way. */
 int stl_comm_sync(void *stream, int timeout_ms);
 /* What RCCL itself reports for the communicator libstl gathers over
  * (ncclCommCount / ncclCommUserRank): the one-process-per-GPU communicator of
@@ -438,7 +442,8 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
 #define STL_TUNE_STREAM_WORKSPACES 6 /* 1..64 (default 4, env STL_MAX_STREAM_WORKSPACES): caller streams
                                         per device whose context (verify workspace ~0.44 GB, hash
                                         queue, checkSign scratch) libstl keeps; the least recently
-                                        used one beyond it is freed */
+                                        used one beyond it is evicted, its buffers kept as a spare
+                                        for the next new caller stream (no device synchronisation) */
 #define STL_TUNE_LONG_HASH 8        /* 0..62 (default 8; 0 off): in calls of at most two lane-pair chunks
                                         (65,536 rows on 256 CUs), up to 1,024 of the longest preimages
                                         of more than this many SHA-512 blocks are hashed one per wave
@@ -449,13 +454,23 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
 int stl_debug_tuning(int key, int value);
 /* Caller-stream contexts libstl currently keeps on the current device. */
 int stl_debug_stream_contexts(void);
+/* Measurement only (bench.py clock_ghz): enqueues nwg one-wave workgroups on
+ * `stream`; workgroup i writes d_out[4i..4i+3] = {shader cycle counter
+ * (s_memtime), 100 MHz counter (s_memrealtime), XCC_ID register, HW_ID
+ * register}.  Two stamps around a timed region give its average shader clock
+ * per XCD.  STL_EINVAL for a null d_out or nwg > 65,536. */
+int stl_debug_clock_stamp(uint64_t *d_out, uint32_t nwg, void *stream);
 
-/* Frees libstl's context of a caller stream on the current device -- its
- * verify workspace, hash queue, checkSign scratch and events -- after a device
- * synchronisation (call it before destroying a stream the library has run
- * on, or let the per-device cap, STL_TUNE_STREAM_WORKSPACES, evict it).  A
- * call still running on that stream keeps the context until it returns.
- * STL_EINVAL for one of libstl's own pool streams; STL_OK if there is none. */
+/* Drops libstl's context of a caller stream on the current device -- its
+ * verify workspace, hash queue, checkSign scratch and events -- without
+ * waiting for anything: the buffers join the device's spare list (at most
+ * STL_TUNE_STREAM_WORKSPACES sets; stl_shutdown frees them), and the next new
+ * caller stream adopts a set, its first kernels ordered on the device behind
+ * the last kernels that used it.  Call it before destroying a stream the
+ * library has run on, or let the per-device cap evict the least recently
+ * used context the same way.  A call still running on that stream keeps the
+ * context until it returns.  STL_EINVAL for one of libstl's own pool streams;
+ * STL_OK if there is none. */
 int stl_release_stream(void *stream);
 
 /* Synthetic-data helpers (RippleAddress::sign, RippleAddress.cpp:254-263;

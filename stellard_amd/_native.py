@@ -103,6 +103,7 @@ SYMBOLS = [
     ("stl_debug_verify_k_device", ctypes.c_int, [_U8P, _U8P, _U8P, ctypes.c_size_t, _P, ctypes.c_uint32, _P]),
     ("stl_debug_tuning", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("stl_debug_stream_contexts", ctypes.c_int, []),
+    ("stl_debug_clock_stamp", ctypes.c_int, [_P, ctypes.c_uint32, _P]),
     ("stl_release_stream", ctypes.c_int, [_P]),
     ("stl_debug_sign_adversarial_device", ctypes.c_int,
      [_U8P, _U8P, _U8P, _P, ctypes.c_size_t, _U8P, _U8P, _U8P, _P]),

@@ -55,13 +55,19 @@ HOST_DEPS = ["stl_kernels.h", os.path.join("..", "..", "include", "stl.h")]
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 
 
-def build_product(force=False, extra_flags=()):
+def build_product(force=False, extra_flags=(), variant="variant"):
     out = os.path.join(ROOT, "stellard_amd", "libstl.so")
     deps = [os.path.join(CSRC, d) for d in PRODUCT_DEPS]
-    if extra_flags:  # variant builds: one command, nothing cached
+    if extra_flags:
+        # variant builds (-D experiment switches): one command, nothing cached,
+        # and never the product's path -- a variant written to libstl.so would
+        # look newer than build/obj and survive the next default build (ADVICE
+        # r5); load one with STL_LIB_PATH=build/ab/<variant>.so
+        vout = os.path.join(ROOT, "build", "ab", variant + ".so")
+        os.makedirs(os.path.dirname(vout), exist_ok=True)
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *extra_flags,
-              "-o", out] + [os.path.join(CSRC, s) for s in PRODUCT_SRCS])
-        return out
+              "-o", vout] + [os.path.join(CSRC, s) for s in PRODUCT_SRCS])
+        return vout
     os.makedirs(OBJ_DIR, exist_ok=True)
     objs = []
     for src in PRODUCT_SRCS:

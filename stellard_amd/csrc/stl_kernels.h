@@ -141,6 +141,8 @@ constexpr size_t kWideTableBytes = 2ull * 32769 * 28 * 4;
 // keys repeat (device-resident automatic dedup; flag may be host-mapped).
 hipError_t launch_key_sample(const uint8_t* pk, uint32_t n, uint32_t* flag, hipStream_t stream);
 hipError_t launch_wide_table(uint4* out, hipStream_t stream);
+// nwg one-wave workgroups, each {memtime, memrealtime, XCC_ID, HW_ID} (4 u64)
+hipError_t launch_clock_stamp(unsigned long long* out, uint32_t nwg, hipStream_t stream);
 // cls / param (nullable, test data only): per-row adversarial class and its
 // parameter (stl_kernels.hip adversarial_row); msg_out receives the messages.
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,

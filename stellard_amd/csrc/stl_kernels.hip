@@ -432,6 +432,33 @@ hipError_t launch_key_sample(const uint8_t* pk, uint32_t n, uint32_t* flag, hipS
   return hipGetLastError();
 }
 
+// Shader-clock stamps (stl_debug_clock_stamp; bench.py's clock_ghz, VERDICT
+// r5 #5): lane 0 of each one-wave workgroup writes the free-running shader
+// cycle counter (s_memtime), the 100 MHz constant-rate counter
+// (s_memrealtime), and the XCC_ID / HW_ID registers naming the XCD, shader
+// engine and CU it ran on.  Two stamps around a timed region give the average
+// shader clock over it as d(memtime) / d(memrealtime) x 100 MHz, taken per
+// XCD (each XCD keeps its own cycle counter).  Vector stores only.
+__global__ __launch_bounds__(64) void clock_stamp_kernel(unsigned long long* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long rt = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  uint32_t xcc, hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  unsigned long long* o = out + 4 * (size_t)blockIdx.x;
+  o[0] = t;
+  o[1] = rt;
+  o[2] = xcc;
+  o[3] = hw;
+}
+
+hipError_t launch_clock_stamp(unsigned long long* out, uint32_t nwg, hipStream_t stream) {
+  if (nwg == 0) return hipSuccess;
+  hipLaunchKernelGGL(clock_stamp_kernel, dim3(nwg), dim3(64), 0, stream, out);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(kBlock) void key_insert_kernel(const uint8_t* __restrict__ pk, uint32_t base,
                                                             uint32_t cnt, uint32_t* __restrict__ slots, uint32_t mask,
                                                             uint32_t* __restrict__ rep, uint32_t* __restrict__ uid_of,

@@ -356,6 +356,12 @@ def signed_blob_verify_batch_device(blobs, offsets, lengths, out_words=None, tx_
     status = torch.empty((n,), dtype=torch.uint8, device=dev) if out_status is None else out_status
     tx_id = out_ids if out_ids is not None else (torch.empty((n, 32), dtype=torch.uint8, device=dev)
                                                  if tx_ids else None)
+    # the kernels write raw bytes: a wider dtype would hold packed bytes the
+    # caller misreads
+    if status.dtype != torch.uint8 or (tx_id is not None and tx_id.dtype != torch.uint8):
+        raise ValueError("out_status / out_ids must be torch.uint8")
+    if tx_id is not None and tx_id.dim() > 1 and tx_id.shape[-1] != 32:
+        raise ValueError("out_ids must be (n, 32) bytes")
     if status.numel() < n or (tx_id is not None and tx_id.numel() < 32 * n):
         raise ValueError("status / id buffers smaller than the batch")
     _check_rows(blobs, offsets, lengths, out_words, status, tx_id)
@@ -621,6 +627,34 @@ def stream_contexts():
     if rc < 0:
         N.check(rc, "stl_debug_stream_contexts")
     return rc
+
+
+def clock_stamp(nwg=256, stream=None):
+    """stl_debug_clock_stamp: (nwg, 4) int64 CUDA tensor of {shader cycle
+    counter, 100 MHz counter, XCC_ID, HW_ID} per one-wave workgroup, enqueued
+    on ``stream`` (bench.py's clock_ghz)."""
+    import torch
+    out = torch.zeros((nwg, 4), dtype=torch.int64, device="cuda")
+    N.check(N.load().stl_debug_clock_stamp(ctypes.c_void_p(out.data_ptr()), nwg, _stream_ptr(stream)),
+            "stl_debug_clock_stamp")
+    return out
+
+
+def clock_ghz(start, end):
+    """Average shader clock (GHz) between two clock_stamp results (numpy or
+    torch (nwg, 4)): per XCD, the median cycle count of its workgroups at each
+    stamp over the median 100 MHz count; returns (median over XCDs, {xcc: GHz})."""
+    a = start.cpu().numpy() if hasattr(start, "cpu") else np.asarray(start)
+    b = end.cpu().numpy() if hasattr(end, "cpu") else np.asarray(end)
+    per = {}
+    for x in sorted(set((a[:, 2] & 0xF).tolist()) & set((b[:, 2] & 0xF).tolist())):
+        sa, sb = a[(a[:, 2] & 0xF) == x], b[(b[:, 2] & 0xF) == x]
+        dt = float(np.median(sb[:, 0]) - np.median(sa[:, 0]))
+        dr = float(np.median(sb[:, 1]) - np.median(sa[:, 1]))
+        if dr > 0:
+            per[int(x)] = dt / dr * 0.1
+    vals = sorted(per.values())
+    return (vals[len(vals) // 2] if vals else None), per
 
 
 def execution_settings():

@@ -120,3 +120,23 @@ def test_flag_validation():
     b = lib.stl_batcher_create(16, 100, N.STL_ONE_LANE)
     assert b
     lib.stl_batcher_destroy(b)
+
+
+def test_blob_call_rejects_wide_status_and_id_buffers():
+    """the blob call's kernels write raw bytes into out_status and
+    out_ids, so a wider dtype (or ids not 32 bytes wide) is refused before any
+    device call -- a caller would otherwise read packed bytes as elements."""
+    torch = pytest.importorskip("torch")
+    from stellard_amd import verify as V
+    n = 4
+    blobs = torch.zeros(64, dtype=torch.uint8)
+    off = torch.zeros(n, dtype=torch.int64)
+    ln = torch.zeros(n, dtype=torch.int32)
+    with pytest.raises(ValueError, match="uint8"):
+        V.signed_blob_verify_batch_device(blobs, off, ln, out_status=torch.zeros(n, dtype=torch.int32))
+    with pytest.raises(ValueError, match="uint8"):
+        V.signed_blob_verify_batch_device(blobs, off, ln, out_status=torch.zeros(n, dtype=torch.uint8),
+                                          out_ids=torch.zeros((n, 4), dtype=torch.int64))
+    with pytest.raises(ValueError, match=r"\(n, 32\)"):
+        V.signed_blob_verify_batch_device(blobs, off, ln, out_status=torch.zeros(n, dtype=torch.uint8),
+                                          out_ids=torch.zeros((n, 64), dtype=torch.uint8))
