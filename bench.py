@@ -254,47 +254,52 @@ def end_to_end(V, torch, sig, msgs, pk, reps=5):
     return out
 
 
-def config1_leg(V, torch, dev, stream, threads_share, n=100_000, nacc=1000, seed=0x5EED0001):
+def config1_leg(V, torch, dev, stream, threads_share):
     """BASELINE configs[0] / SURVEY 8d config 1: 100,000 synthetic Payment
     transactions of 1,000 accounts as whole serialized blobs (Appendix C,
-    175-220 B), checkSign from the bytes: libstl's device-resident
-    stl_tx_blob_prepare_device + verify, its host API stl_tx_blob_verify_batch
-    (PCIe-inclusive), and the reference's own path on the host CPUs --
-    parse, re-serialise, OpenSSL SHA-512, libsodium verify && S<L
-    (SerializedTransaction.cpp:220-230, Serializer.cpp:354-360,
+    175-221 B; tests/datasets.py config1_plan: tools/payments.py's rows, 2 %
+    of them invalid -- payload / R / S bits flipped after signing, Flags and
+    Sequence swapped (DEFERRED), 33-byte keys (MALFORMED)), checkSign from the
+    bytes: libstl's device-resident one call stl_signed_blob_verify_batch_device,
+    the two-step stl_tx_blob_prepare_device + verify, its host API
+    stl_tx_blob_verify_batch (PCIe-inclusive), and the reference's own path on
+    the host CPUs -- parse, re-serialise, OpenSSL SHA-512, libsodium verify &&
+    S<L (SerializedTransaction.cpp:220-230, Serializer.cpp:354-360,
     RippleAddress.cpp:190-200; oracle/_ref/libsodium_ref.so's
-    ref_tx_blob_verify_batch) at T = affinity / box share / 6 / 1."""
+    ref_tx_blob_verify_batch) at T = affinity / box share / 6 / 1.  Bits,
+    status bytes and ids are compared with the committed reference digests
+    (tests/golden/make_digests.py config1)."""
     import ctypes
-    from tests import oracle_bind
-    from tools.payments import blobs_from_preimages, pack, payment_preimages
+    import hashlib
+    from tests import datasets, oracle_bind
     from stellard_amd import _native as N
-    rng = np.random.default_rng(seed)
-    acc_seeds = rng.integers(0, 256, (nacc, 32), dtype=np.uint8)
-    apk, _ = V.sign_batch_device(torch.from_numpy(acc_seeds).to(dev), torch.zeros((nacc, 32), dtype=torch.uint8,
-                                                                                    device=dev))
-    apk = apk.cpu().numpy()
-    pre = payment_preimages(apk, n, rng)
-    pbuf, poff, plen = pack(pre)
-    d_msg = V.tx_hash_batch_device(torch.from_numpy(pbuf).to(dev), torch.from_numpy(poff.view(np.int64)).to(dev),
-                                   torch.from_numpy(plen.view(np.int32)).to(dev), stream=stream)
-    seeds = torch.from_numpy(acc_seeds[np.arange(n) % nacc]).to(dev)
-    tpk, tsig = V.sign_batch_device(seeds, d_msg)
-    torch.cuda.synchronize()
-    blobs = blobs_from_preimages(pre, tsig.cpu().numpy(), tpk.cpu().numpy())
-    buf, offs, lens = pack(blobs)
-    buf = np.concatenate([buf, np.zeros(4, np.uint8)])
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)["config1"]
+
+    def signer_pks(seeds):
+        z = torch.zeros((seeds.shape[0], 32), dtype=torch.uint8, device=dev)
+        return V.sign_batch_device(torch.from_numpy(np.ascontiguousarray(seeds)).to(dev), z)[0].cpu().numpy()
+    plan = datasets.config1_plan(signer_pks)
+    n, nacc = plan["n"], datasets.CONFIG1["accounts"]
+    msgs = torch.from_numpy(datasets.config1_signing_hashes(plan)).to(dev)
+    _, tsig = V.sign_batch_device(torch.from_numpy(np.ascontiguousarray(plan["seeds"][plan["who"]])).to(dev), msgs)
+    buf, offs, lens = datasets.config1_finish(plan, tsig.cpu().numpy())
+    inputs_ok = datasets.config1_inputs_h16(buf, lens) == want["inputs_h16"]
     d_buf = torch.from_numpy(buf).to(dev)
-    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
-    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_len = torch.from_numpy(lens).to(dev)
     words = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
 
     def two_step():
         o = V.tx_blob_prepare_device(d_buf, d_off, d_len, tx_ids=False, stream=stream)
         V.verify_batch_device(o["sig"], o["msg"], o["pk"], out_words=words, stream=stream)
         return o
 
-    def one_call():  # stl_tx_blob_verify_batch_device: the blob pass and verify chunked over two streams
-        return V.signed_blob_verify_batch_device(d_buf, d_off, d_len, out_words=words, stream=stream)
+    def one_call():  # stl_signed_blob_verify_batch_device: the blob pass and verify chunked over two streams
+        return V.signed_blob_verify_batch_device(d_buf, d_off, d_len, out_words=words, out_status=status,
+                                                 stream=stream)
 
     def med(fn, reps=7):
         fn()
@@ -310,15 +315,23 @@ def config1_leg(V, torch, dev, stream, threads_share, n=100_000, nacc=1000, seed
     two_s = med(two_step)
     two_bits = V.words_to_bool(words, n)
     dev_s = med(one_call)
-    o = one_call()
+    o = V.signed_blob_verify_batch_device(d_buf, d_off, d_len, out_words=words, tx_ids=True, stream=stream)
     torch.cuda.synchronize()
     dev_bits = V.words_to_bool(words, n)
-    status_ok = int((o["status"].cpu().numpy() == V.TX_OK).sum())
+    dev_status = o["status"].cpu().numpy()
+    digests = {"inputs_equal": inputs_ok,
+               "bitmap_equal": sha(np.packbits(dev_bits, bitorder="little")) == want["bitmap_sha256"],
+               "status_equal": sha(dev_status) == want["status_sha256"],
+               "ids_equal": sha(o["tx_id"].cpu().numpy()) == want["ids_sha256"],
+               "accepted": int(dev_bits.sum()), "accepted_expected": want["accepted"],
+               "expected_from": "tests/golden/bitmap_digests.json config1 (make_digests.py: re-serialise + "
+                                "OpenSSL + libsodium per row, here in the build container)"}
     B = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     bm = np.zeros((n + 7) // 8, np.uint8)
     st = np.zeros(n, np.uint8)
+    o64, l32 = offs.astype(np.uint64), lens.astype(np.uint32)
     lib = N.load()
-    host = lambda: N.check(lib.stl_tx_blob_verify_batch(B(buf), B(offs), B(lens), n, B(bm), B(st), None, 0),  # noqa: E731
+    host = lambda: N.check(lib.stl_tx_blob_verify_batch(B(buf), B(o64), B(l32), n, B(bm), B(st), None, 0),  # noqa: E731
                            "stl_tx_blob_verify_batch")
     host()
     ts = []
@@ -328,11 +341,15 @@ def config1_leg(V, torch, dev, stream, threads_share, n=100_000, nacc=1000, seed
         ts.append(time.perf_counter() - t0)
     host_s = float(np.median(ts))
     host_bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    digests["host_api_bitmap_equal"] = sha(bm) == want["bitmap_sha256"]
+    digests["host_api_status_equal"] = sha(st) == want["status_sha256"]
     out = {"n": n, "accounts": nacc, "blob_bytes": {"min": int(lens.min()), "median": int(np.median(lens)),
                                                    "max": int(lens.max())},
+           "invalid_rows": int(plan["bad"].size),
            "gpu_device_resident_tx_per_s": n / dev_s, "gpu_device_ms": dev_s * 1e3,
            "gpu_device_two_step_tx_per_s": n / two_s, "two_step_bits_equal": bool((two_bits == dev_bits).all()),
-           "gpu_host_api_tx_per_s": n / host_s, "gpu_host_api_ms": host_s * 1e3, "status_ok": status_ok,
+           "gpu_host_api_tx_per_s": n / host_s, "gpu_host_api_ms": host_s * 1e3,
+           "status_ok": int((dev_status == V.TX_OK).sum()), "digests": digests,
            "gpu_timing": "host clock around one stl_signed_blob_verify_batch_device call + sync (device-resident; "
                          "two_step: stl_tx_blob_prepare_device + stl_ed25519_verify_batch_device), or around one "
                          "stl_tx_blob_verify_batch call (host API); median"}
@@ -340,6 +357,7 @@ def config1_leg(V, torch, dev, stream, threads_share, n=100_000, nacc=1000, seed
     if lib_ref is None:
         out["cpu_reference"] = None
         return out
+    blobs = [buf[int(a):int(a) + int(b)].tobytes() for a, b in zip(offs, lens)]
     cpu = {}
     ref_bits = None
     for t, cap in ((affinity_cpus(), n), (threads_share, n), (JOBQUEUE_THREADS, 50_000), (1, 10_000)):
@@ -361,9 +379,13 @@ def config1_leg(V, torch, dev, stream, threads_share, n=100_000, nacc=1000, seed
                                     "OpenSSL SHA512 + libsodium 1.0.18 crypto_sign_verify_detached && S<L, "
                                     "std::thread-style static partition, median of 3"}
     if ref_bits is not None:
-        out["bitmap_parity"] = {"rows": n, "accepted": int(ref_bits.sum()),
-                                "mismatches_device": int((dev_bits != ref_bits).sum()),
-                                "mismatches_host_api": int((host_bits != ref_bits).sum())}
+        # the device contract: the reference's bit where the row's status is
+        # OK; deferred rows (the reference accepts them) go to the caller
+        ok = dev_status == V.TX_OK
+        out["bitmap_parity"] = {"rows": n, "reference_accepted": int(ref_bits.sum()),
+                                "mismatches_device": int((dev_bits != (ref_bits & ok)).sum()),
+                                "mismatches_host_api": int((host_bits != (ref_bits & ok)).sum()),
+                                "deferred_rows_reference_accepts": int((ref_bits & (dev_status == V.TX_DEFERRED)).sum())}
     return out
 
 
@@ -554,6 +576,10 @@ def gpu_run(args, world, rank, local):
         raise SystemExit(f"rank {rank}: {int((~ok).sum())} valid signatures rejected -- parity failure")
 
     # ---- timed region: exactly K steps between barrier+sync on both sides ----
+    # shader-clock stamps (stl_debug_clock_stamp) right before and right after
+    # it, both outside it: the chip's average clock over the timed launches
+    # (boxes hold 2.1-2.3 GHz under this load)
+    clk0 = V.clock_stamp(256, stream)
     torch.cuda.synchronize()
     V.set_phase_timing(False)
     V.reset_stats()
@@ -571,6 +597,9 @@ def gpu_run(args, world, rank, local):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    clk1 = V.clock_stamp(256, stream)
+    torch.cuda.synchronize()
+    clock_ghz, clock_xcc, clock_cus = V.clock_ghz(clk0, clk1)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     t = torch.tensor([dt, kern_ms], dtype=torch.float64)
     if world > 1:
@@ -657,6 +686,13 @@ def gpu_run(args, world, rank, local):
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / args.steps,
+            "clock_ghz": clock_ghz,
+            "cycles_per_verify": (dt / args.steps) * clock_ghz * 1e9 / n if clock_ghz else None,
+            "clock": {"per_xcc_ghz": clock_xcc, "cus_matched": clock_cus,
+                      "how": "stl_debug_clock_stamp (one wave per workgroup, 256 workgroups) right before and "
+                             "right after the timed region: per CU, d(s_memtime) / d(s_memrealtime) x 100 MHz, "
+                             "median over the CUs stamped both times (rank 0's GPU); cycles_per_verify = "
+                             "ms_per_step x clock_ghz / signatures per GPU"},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -279,6 +279,13 @@ std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even
 std::atomic<int> g_tune_quad{3};      // smallest chunks' main kernel on lane groups: bit 0 quads, bit 1 duos
 std::atomic<int> g_tune_long_hash{8}; // small batches: rows of more than this many blocks hashed one per wave (0 off)
 
+// Rows per step of verify time: the device-resident verify runs a chunk's
+// 64-signature units on its resident waves, two per SIMD, so its time rises in
+// steps of one wave per SIMD (65,536 rows on 256 CUs): a
+// shard one row past a multiple pays a whole extra step on its slowest SIMDs.
+// Set at stl_init from the first device; 65,536 (MI355X) before that.
+std::atomic<uint64_t> g_shard_quantum{65536};
+
 // Chunk size of a device-resident call of n signatures over several streams
 // (DESIGN.md section 4): round(n / 2^18) chunks, at least two, of equal size
 // (a multiple of 64, above the lane-pair size), so a mid-size batch still has
@@ -567,6 +574,7 @@ int setup_device(Device& d) {
   STL_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stl::kernel_verify_msg32(), stl::kBlock, 0));
   if (per_cu < 1) per_cu = 1;
   d.grid = (uint32_t)(d.cus * per_cu);
+  g_shard_quantum.store((uint64_t)d.grid * stl::kBlock / 2);  // one verify wave per SIMD
   // the stream pool, in this order (see Device)
   STL_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   STL_TRY(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
@@ -841,19 +849,43 @@ void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
   *hi = std::min(n, (size_t)(r + 1) * per * 64);
 }
 
+
 // Byte-balanced 64-aligned shard boundaries: bound[r] = the 64-aligned row at
-// or after the first row whose byte prefix sum reaches r/g of the total.
+// or after the first row whose byte prefix sum reaches r/g of the total --
+// then moved to the nearest multiple of g_shard_quantum rows when that moves
+// its byte prefix by at most 1 % of one rank's share (config 5's
+// 2^20-row ledger over 8 ranks byte-balances to 130,304-131,584 rows, and the
+// ranks past 131,072 paid a sliver of a second round; equal rows cost the
+// ranks at most 0.6 % of bytes, i.e. of the ~20 % of a rank's time that is
+// hashing).  tests/test_multigpu_host.py holds the Python mirror to it.
 void shard_bytes_bounds(const uint32_t* len, size_t n, int g, std::vector<size_t>& bound) {
   bound.assign(g + 1, n);
   bound[0] = 0;
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i) total += len[i];
+  const uint64_t q = g_shard_quantum.load();
   uint64_t acc = 0;
   size_t i = 0;
   for (int r = 1; r < g; ++r) {
     const uint64_t target = (uint64_t)((__uint128_t)total * (unsigned)r / (unsigned)g);
     while (i < n && acc < target) acc += len[i++];
-    const size_t b = std::min(n, (i + 63) / 64 * 64);
+    size_t b = std::min(n, (i + 63) / 64 * 64);
+    if (q >= 64 && q % 64 == 0 && n > q) {
+      // the byte prefix at row b (acc is the prefix at row i <= b)
+      auto prefix = [&](size_t row) {
+        uint64_t p = acc;
+        if (row >= i)
+          for (size_t k = i; k < row; ++k) p += len[k];
+        else
+          for (size_t k = row; k < i; ++k) p -= len[k];
+        return p;
+      };
+      const size_t down = b / q * q, up = down + q;
+      const size_t c = (b - down <= up - b || up > n) ? down : up;
+      const uint64_t pc = prefix(c);
+      const uint64_t dev = pc > target ? pc - target : target - pc;
+      if (c > 0 && c < n && (__uint128_t)dev * (unsigned)g * 100u <= (__uint128_t)total) b = c;
+    }
     bound[r] = std::max(bound[r - 1], b);
   }
 }

@@ -488,7 +488,8 @@ __global__ __launch_bounds__(kBlock) void key_insert_kernel(const uint8_t* __res
     }
     rep[t] = r;
   }
-  // compact ids for the owners: one atomic per wave
+  // compact ids for the owners: one atomic per wave (no loop: the broadcast
+  // base only offsets each owner lane's own id)
   const bool owner = live && r == t;
   const uint64_t m = __ballot(owner);
   if (m == 0) return;
@@ -720,6 +721,13 @@ __global__ __launch_bounds__(kBlock, STL_VERIFY_WAVES_PER_SIMD) void verify_main
   uint32_t unit = blockIdx.x * (kBlock / 64) + wave;
   for (;;) {
     if (queue) {  // wave-uniform: one atomic per wave and unit
+      // The claimed unit is broadcast with readfirstlane, so it lives in an
+      // SGPR and the exit test below is a scalar compare (s_cmp + s_cbranch_scc
+      // in the ISA): the loop is uniform control flow whose back-edge always
+      // passes through the claim.  A VGPR broadcast (__shfl) would make the
+      // exit test a VGPR compare that the structuriser may split into nested
+      // exec-masked loops, one of them not re-running the claim (DESIGN.md
+      // section 4, "Work queues": the round-5 long-row hang).
       uint32_t u = 0;
       if (lane == 0) u = atomicAdd(queue, 1u);
       unit = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
@@ -1340,7 +1348,12 @@ __device__ __forceinline__ void hash_long_rows(const uint8_t* __restrict__ pre, 
   uint2* wsch = reinterpret_cast<uint2*>(win);
   // rows r = wave, wave + waves, ... < K: a static deal (the rows are the
   // longest of the batch, about equal), every index a scalar, so the row loop
-  // is uniform control flow
+  // is uniform control flow (s_cmp / s_cbranch_scc on K, r in the ISA).  A
+  // dynamic deal -- lane 0 claiming the row with an atomic, __shfl broadcasting
+  // it -- hung in round 5: the index was a VGPR, and in the ISA of a rebuilt
+  // form of it the claim sits in an outer loop's header while the broadcast,
+  // the exit test and the body form a nested exec-masked loop that iterates
+  // without re-claiming ("Work queues").
   const uint32_t K = __builtin_amdgcn_readfirstlane(counter[2]);
   const uint32_t waves = gridDim.x * (kBlock / 64u);
   const uint32_t first = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6));
@@ -1425,6 +1438,12 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_hash_kerne
   uint32_t mi = 0, blk = 0, nb = 0;
   bool active = false, exhausted = false;
   for (;;) {
+    // Work queue, per lane: the leader claims one row for every idle lane and
+    // __shfl hands the base to all of them (a VGPR, by design: each lane then
+    // takes its own row, so the rows ARE divergent).  The loop's exit is the
+    // ballot `__any(active)` below -- a scalar of the whole wave -- so no lane
+    // can stay in the loop on a stale claim, and a lane that found the queue
+    // empty simply idles until the wave leaves.
     const uint64_t need = __ballot(!active);
     if (need != 0 && !exhausted) {  // wave-uniform
       const int leader = __ffsll((unsigned long long)need) - 1;
@@ -1640,6 +1659,8 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
   const uint8_t* bend = blobs;
   bool active = false, exhausted = false;
   for (;;) {
+    // the per-lane work queue of tx_hash_kernel (each lane its own row, the
+    // loop left on the wave-wide ballot below)
     const uint64_t need = __ballot(!active);
     if (need != 0 && !exhausted) {  // wave-uniform
       const int leader = __ffsll((unsigned long long)need) - 1;

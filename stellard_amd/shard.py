@@ -18,27 +18,42 @@ def shard_range(n, rank, world):
     return lo, hi
 
 
-def shard_range_bytes(lens, rank, world):
+# Rows per step of the device-resident verify time (one main-kernel wave per
+# SIMD: 256 CUs x 4 SIMDs x 64 lanes on MI355X); stl_api.cpp g_shard_quantum
+QUANTUM = 65536
+
+
+def shard_range_bytes(lens, rank, world, quantum=QUANTUM):
     """Byte-balanced shard (same as stl_api.cpp shard_bytes_bounds /
     stl_shard_range_bytes): boundary r is the 64-aligned row at or after the
-    first row where the byte prefix sum reaches r/world of the total.
-    Variable-length rows (config 5: 100 B - 4 KB preimages) cost in
-    proportion to their SHA-512 blocks, so ranks get equal bytes, not equal
-    counts."""
+    first row where the byte prefix sum reaches r/world of the total, moved to
+    the nearest multiple of ``quantum`` rows when that moves its byte prefix by
+    at most 1 % of one rank's share.  Variable-length rows (config 5: 100 B -
+    4 KB preimages) cost in proportion to their SHA-512 blocks, so ranks get
+    equal bytes, not equal counts -- but the verify time rises in steps of
+    ``quantum`` rows, so a shard just past a step is pulled back to it."""
     lens = np.asarray(lens, dtype=np.uint64)
     n = lens.shape[0]
+    total = int(lens.sum())
+    csum = np.concatenate([np.zeros(1, np.uint64), np.cumsum(lens, dtype=np.uint64)])  # csum[i] = sum(lens[:i])
 
     def bound(r):
         if r <= 0:
             return 0
         if r >= world:
             return n
-        total = int(lens.sum())
         target = total * r // world
-        csum = np.cumsum(lens, dtype=np.uint64)
         # smallest i with prefix(i) = sum(lens[:i]) >= target
-        i = 0 if target == 0 else int(np.searchsorted(csum, target, side="left")) + 1
-        return min(n, (i + 63) // 64 * 64)
+        i = 0 if target == 0 else int(np.searchsorted(csum[1:], target, side="left")) + 1
+        b = min(n, (i + 63) // 64 * 64)
+        q = quantum
+        if q >= 64 and q % 64 == 0 and n > q:
+            down = b // q * q
+            up = down + q
+            c = down if (b - down <= up - b or up > n) else up
+            if 0 < c < n and abs(int(csum[c]) - target) * world * 100 <= total:
+                b = c
+        return b
 
     b = [bound(0)]
     for r in range(1, world + 1):

@@ -642,19 +642,33 @@ def clock_stamp(nwg=256, stream=None):
 
 def clock_ghz(start, end):
     """Average shader clock (GHz) between two clock_stamp results (numpy or
-    torch (nwg, 4)): per XCD, the median cycle count of its workgroups at each
-    stamp over the median 100 MHz count; returns (median over XCDs, {xcc: GHz})."""
+    torch (nwg, 4)).  Each CU keeps its own cycle counter (tools/clock_probe.py:
+    counters of one XCD differ by ~1e8 cycles at one instant), so stamps are
+    matched per CU -- XCC_ID and HW_ID bits 8-15 (CU, SH, SE) -- and the clock
+    of each CU is its cycle delta over its 100 MHz delta.  Returns (median over
+    the CUs found in both stamps, {xcc: median over its CUs}, CUs matched)."""
     a = start.cpu().numpy() if hasattr(start, "cpu") else np.asarray(start)
     b = end.cpu().numpy() if hasattr(end, "cpu") else np.asarray(end)
-    per = {}
-    for x in sorted(set((a[:, 2] & 0xF).tolist()) & set((b[:, 2] & 0xF).tolist())):
-        sa, sb = a[(a[:, 2] & 0xF) == x], b[(b[:, 2] & 0xF) == x]
-        dt = float(np.median(sb[:, 0]) - np.median(sa[:, 0]))
-        dr = float(np.median(sb[:, 1]) - np.median(sa[:, 1]))
+
+    def by_cu(x):
+        d = {}
+        for t, rt, xcc, hw in x.tolist():
+            d.setdefault((int(xcc) & 0xF, (int(hw) >> 8) & 0xFF), []).append((t, rt))
+        return {k: (float(np.median([v[0] for v in vs])), float(np.median([v[1] for v in vs])))
+                for k, vs in d.items()}
+    sa, sb = by_cu(a), by_cu(b)
+    per_cu = {}
+    for k in sorted(set(sa) & set(sb)):
+        dr = sb[k][1] - sa[k][1]
         if dr > 0:
-            per[int(x)] = dt / dr * 0.1
-    vals = sorted(per.values())
-    return (vals[len(vals) // 2] if vals else None), per
+            per_cu[k] = (sb[k][0] - sa[k][0]) / dr * 0.1
+    if not per_cu:
+        return None, {}, 0
+    per_xcc = {}
+    for (xcc, _), v in per_cu.items():
+        per_xcc.setdefault(xcc, []).append(v)
+    vals = sorted(per_cu.values())
+    return vals[len(vals) // 2], {x: float(np.median(v)) for x, v in sorted(per_xcc.items())}, len(per_cu)
 
 
 def execution_settings():

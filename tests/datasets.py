@@ -548,3 +548,87 @@ def blob_ledger_cpu(oracle, n, frac=0.05, seed=0x5EED0007):
     blob_ledger_finish(bp, sig)
     buf, offs, lens = bp["buf"], bp["offs"], bp["lens"]
     return bp, [bytes(buf[int(o):int(o) + int(ln)]) for o, ln in zip(offs, lens)]
+
+
+# ---- configs[0]: 100k Payment blobs ----------------------
+# bench.py's config-1 leg construction (tools/payments.py: seed 0x5EED0001,
+# 1,000 accounts, ~175-220-byte Payment transactions, every account signing in
+# turn), plus 2 % invalid rows of the BLOB_KINDS, drawn from a second seeded
+# generator so the valid rows are the bench leg's:
+#   0 payload_bit     a Destination bit flipped after signing    -> reject
+#   1 R_bit / 2 S_bit a signature bit flipped after signing      -> reject
+#   3 deferred_order  Flags and Sequence swapped after signing   -> DEFERRED
+#                     (the reference re-serialises and accepts)
+#   4 malformed_pk33  a 33-byte SigningPubKey, signed over its own preimage
+#                     -> checkSign false (RippleAddress.cpp:192-194), MALFORMED
+CONFIG1 = {"n": 100_000, "seed": 0x5EED0001, "accounts": 1000, "frac": 0.02, "bad_seed": 0x5EED0B01}
+
+
+def config1_plan(signer_pks, cfg=CONFIG1):
+    """The unsigned configs[0] set: signing preimages ('STX\\0' || fields)
+    with the malformed rows' 33-byte keys already in, each row's signer, the
+    invalid rows.  signer_pks(seeds (a,32)) -> (a,32) public keys (the device
+    signer on the box, libsodium here -- the same bytes)."""
+    from tools.payments import payment_preimages
+    rng = np.random.default_rng(cfg["seed"])
+    nacc, n = cfg["accounts"], cfg["n"]
+    seeds = rng.integers(0, 256, (nacc, 32), dtype=np.uint8)
+    pks = np.ascontiguousarray(signer_pks(seeds), np.uint8)
+    pre = payment_preimages(pks, n, rng)
+    who = np.arange(n) % nacc
+    r2 = np.random.default_rng(cfg["bad_seed"])
+    bad = np.sort(r2.choice(n, int(n * cfg["frac"]), replace=False))
+    kind = (np.arange(bad.size) % len(BLOB_KINDS)).astype(np.uint8)
+    param = r2.integers(0, 1 << 32, bad.size, dtype=np.uint64)
+    for i, u in zip(bad[kind == 4], param[kind == 4]):
+        p = pre[i]
+        k = p.index(b"\x73\x20" + pks[who[i]].tobytes())
+        pre[i] = p[:k] + b"\x73\x21" + p[k + 2:k + 34] + bytes([int(u) & 0xFF]) + p[k + 34:]
+    return {"n": n, "pre": pre, "seeds": seeds, "pks": pks, "who": who, "bad": bad, "kind": kind, "param": param}
+
+
+def config1_signing_hashes(plan):
+    """SHA512Half of every signing preimage (hashlib, on the host)."""
+    return np.frombuffer(b"".join(hashlib.sha512(p).digest()[:32] for p in plan["pre"]), np.uint8).reshape(-1, 32)
+
+
+def config1_finish(plan, sig):
+    """The serialized blobs: each preimage without 'STX\\0' with TxnSignature
+    (0x74 0x40 + 64 B) after SigningPubKey, as STObject::add(s, true) orders
+    them; then the post-signing mutations of kinds 0-3.  -> (buf, offs, lens)
+    packed with a 16-byte zero tail (the kernels' loads)."""
+    blobs = []
+    fee = b"\x68\x40\x00\x00\x00\x00\x00\x00\x0a"  # Fee (10 drops), right before SigningPubKey
+    for i, p in enumerate(plan["pre"]):
+        k = p.index(fee) + 9
+        assert p[k] == 0x73, i
+        k += 2 + p[k + 1]
+        blobs.append(bytearray(p[4:k] + b"\x74\x40" + bytes(sig[i]) + p[k:]))
+    for i, kd, u in zip(plan["bad"], plan["kind"], plan["param"]):
+        b, u = blobs[i], int(u)
+        bit = 1 << ((u >> 16) & 7)
+        s = b.index(b"\x74\x40") + 2
+        if kd == 0:
+            b[len(b) - 20 + u % 20] ^= bit  # Destination, the last field
+        elif kd == 1:
+            b[s + u % 32] ^= bit
+        elif kd == 2:
+            b[s + 32 + u % 32] ^= bit
+        elif kd == 3:
+            b[3:8], b[8:13] = b[8:13], b[3:8]  # Flags (0x22 ..) <-> Sequence (0x24 ..)
+    lens = np.array([len(b) for b in blobs], np.int32)
+    offs = np.zeros(len(blobs), np.int64)
+    offs[1:] = np.cumsum(lens[:-1])
+    buf = np.frombuffer(b"".join(bytes(b) for b in blobs) + bytes(16), np.uint8).copy()
+    return buf, offs, lens
+
+
+def config1_inputs_h16(buf, lens):
+    return h16(buf[:int(lens.astype(np.int64).sum())], lens.astype("<i4"))
+
+
+def config1_expected_status(plan):
+    st = np.zeros(plan["n"], np.uint8)
+    st[plan["bad"][plan["kind"] == 3]] = 1
+    st[plan["bad"][plan["kind"] == 4]] = 2
+    return st

@@ -12,7 +12,7 @@ box.  Signing and verification both go through oracle/_ref/libsodium_ref.so
 (crypto_sign_seed_keypair + crypto_sign_detached, and the reference's
 verifySignature = crypto_sign_verify_detached && S < L).
 
-    python tests/golden/make_digests.py [config2 config4 config3 config5 config5b]
+    python tests/golden/make_digests.py [config2 config4 config3 config5 config5b config1]
 """
 import json
 import os
@@ -147,6 +147,73 @@ def config5b(lib, threads):
                              "SHA512Half('TXN\\0' || blob), zero for deferred rows"}
 
 
+def config1(lib, threads):
+    """configs[0]: the 100k Payment blobs of
+    datasets.config1_plan -- bench.py's config-1 rows plus 2 % invalid rows
+    (datasets.BLOB_KINDS) -- signed with libsodium over hashlib's SHA512Half of
+    each signing preimage, then the reference's checkSign of every row: parse,
+    re-serialise (oracle/stl_oracle_tx.c), OpenSSL SHA-512, libsodium verify &&
+    S < L (ref_tx_blob_verify_batch), each row's status from the same
+    re-serialiser, and the transaction ids."""
+    import ctypes
+    import hashlib
+    zeros = lambda s: oracle_bind.sodium_sign_batch(lib, s, np.zeros((s.shape[0], 32), np.uint8), threads)[0]  # noqa: E731
+    plan = datasets.config1_plan(zeros)
+    n = plan["n"]
+    msgs = datasets.config1_signing_hashes(plan)
+    pk, sig = oracle_bind.sodium_sign_batch(lib, np.ascontiguousarray(plan["seeds"][plan["who"]]), msgs, threads)
+    assert np.array_equal(pk, plan["pks"][plan["who"]])
+    buf, offs, lens = datasets.config1_finish(plan, sig)
+    offs, lens = offs.astype(np.uint64), lens.astype(np.uint32)
+    B = oracle_bind._buf
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    ids = np.zeros((n, 32), np.uint8)
+    lib.ref_tx_blob_verify_batch(B(buf), B(offs), B(lens), n, B(bm), B(ids), 0, threads)
+    ref_bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    orc = oracle_bind.load_oracle()
+    mv = memoryview(buf)
+    status = np.zeros(n, np.uint8)
+    cap = int(lens.max()) + 64
+    sb, fb = ctypes.create_string_buffer(cap), ctypes.create_string_buffer(cap)
+    info = oracle_bind.TxInfo()
+    for i in range(n):
+        b = mv[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+        ok = orc.lib.oracle_tx_blob(b, len(b), sb, fb, cap, ctypes.byref(info)) == 0
+        assert ok, ("reference cannot construct row", i)
+        if fb.raw[:info.full_len] != b:
+            status[i] = 1
+        elif info.pk_len != 32 or info.sig_len != 64:
+            status[i] = 2
+    want_st = datasets.config1_expected_status(plan)
+    assert np.array_equal(status, want_st), np.nonzero(status != want_st)[0][:10]
+    kinds = {k: plan["bad"][plan["kind"] == i] for i, k in enumerate(datasets.BLOB_KINDS)}
+    for k in ("payload_bit", "R_bit", "S_bit", "malformed_pk33"):
+        assert not ref_bits[kinds[k]].any(), k
+    assert ref_bits[kinds["deferred_order"]].all()
+    assert ref_bits.sum() == n - plan["bad"].size + kinds["deferred_order"].size
+    dev_bits = ref_bits & (status == 0)
+    ids[status == 1] = 0  # the device writes no id for a deferred row
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    return {"rows": n, "accepted": int(dev_bits.sum()),
+            "bitmap_sha256": sha(np.packbits(dev_bits, bitorder="little")),
+            "ref_accepted": int(ref_bits.sum()), "ref_bitmap_sha256": sha(np.packbits(ref_bits, bitorder="little")),
+            "status_sha256": sha(status), "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
+            "ids_sha256": sha(ids), "inputs_h16": datasets.config1_inputs_h16(buf, lens),
+            "blob_bytes": int(lens.astype(np.int64).sum()),
+            "blob_len": {"min": int(lens.min()), "median": int(np.median(lens)), "max": int(lens.max())},
+            "invalid_rows": int(plan["bad"].size),
+            "invalid_by_kind": {k: int(v.size) for k, v in kinds.items()},
+            **{k: v for k, v in datasets.CONFIG1.items()},
+            "construction": "datasets.config1_plan: bench.py's config-1 Payment transactions (tools/payments.py, "
+                            "1,000 accounts signing in turn) as serialized blobs, signed over SHA512Half('STX\\0' "
+                            "|| preimage fields), 2 % invalid rows made after signing (datasets.BLOB_KINDS; the "
+                            "33-byte keys before it)",
+            "expected_from": f"reference checkSign per row: oracle/stl_oracle_tx.c parse + re-serialise, OpenSSL "
+                             f"SHA-512, libsodium {lib.ref_sodium_version().decode()} crypto_sign_verify_detached "
+                             "&& S < L (ref_tx_blob_verify_batch); bitmap_sha256 = that && status OK; ids_sha256 = "
+                             "SHA512Half('TXN\\0' || blob), zero for deferred rows"}
+
+
 def main(names):
     lib = oracle_bind.load_sodium_ref()
     assert lib is not None, "needs libsodium"
@@ -158,8 +225,8 @@ def main(names):
     group = datasets.sodium_group(lib)
     for name in names:
         t0 = time.time()
-        if name in ("config5", "config5b"):
-            got = (config5 if name == "config5" else config5b)(lib, threads)
+        if name in ("config5", "config5b", "config1"):
+            got = {"config5": config5, "config5b": config5b, "config1": config1}[name](lib, threads)
             _check_same(out, name, got)
             out[name] = got
             with open(datasets.DIGESTS, "w") as f:
@@ -203,4 +270,4 @@ def main(names):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["config2", "config4", "config3", "config5", "config5b"])
+    main(sys.argv[1:] or ["config2", "config4", "config3", "config5", "config5b", "config1"])

@@ -100,3 +100,31 @@ def test_plan_even_and_distinct(name):
     cls, param = first
     adv = np.nonzero(cls)[0]
     assert np.unique(param[adv]).size > 0.99 * adv.size  # parameters drawn per row
+
+
+def test_config1_construction_reproduces_committed_digest(sodium):
+    """configs[0]: datasets.config1_plan + libsodium signing
+    rebuilds exactly the inputs make_digests.py config1 committed, the invalid
+    rows are 2 % split evenly over datasets.BLOB_KINDS, and the valid rows are
+    bench.py's earlier config-1 rows (the same tools/payments.py draws); the
+    reference's checkSign (ref_tx_blob_verify_batch: re-serialise + OpenSSL +
+    libsodium) rejects every payload / R / S / 33-byte-key row and accepts the
+    rest, the reordered rows included."""
+    import json
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)["config1"]
+    zeros = lambda s: oracle_bind.sodium_sign_batch(sodium, s, np.zeros((s.shape[0], 32), np.uint8), 8)[0]  # noqa: E731
+    plan = datasets.config1_plan(zeros)
+    msgs = datasets.config1_signing_hashes(plan)
+    pk, sig = oracle_bind.sodium_sign_batch(sodium, np.ascontiguousarray(plan["seeds"][plan["who"]]), msgs, 8)
+    buf, offs, lens = datasets.config1_finish(plan, sig)
+    assert datasets.config1_inputs_h16(buf, lens) == want["inputs_h16"]
+    counts = np.bincount(plan["kind"], minlength=len(datasets.BLOB_KINDS))
+    assert plan["bad"].size == 2000 and (counts == 400).all()
+    assert 175 <= lens.min() and lens.max() <= 221
+    blobs = [buf[int(a):int(a) + int(b)].tobytes() for a, b in zip(offs, lens)]
+    bits = oracle_bind.sodium_tx_blob_verify_batch(sodium, blobs, threads=8)
+    expect = np.ones(plan["n"], bool)
+    rej = plan["bad"][plan["kind"] != 3]
+    expect[rej] = False
+    assert np.array_equal(bits, expect)

@@ -303,3 +303,55 @@ def test_checksign_long_mode_same_bits(stl, torch_cuda, ledger):
             assert np.array_equal(bits[1], expect), (lo, m)
     finally:
         stl.debug_tuning(stl.TUNE_LONG_HASH, old)
+
+
+@pytest.mark.timeout(300)
+def test_config1_payment_blobs_digests(stl, torch_cuda):
+    """VERDICT r5 #2, configs[0] pinned in the GPU suite: the 100k Payment
+    blobs of datasets.config1_plan (bench.py's config-1 rows + 2 % invalid:
+    payload / R / S bits flipped after signing, Flags-Sequence swapped ->
+    DEFERRED, 33-byte keys -> MALFORMED) rebuilt with the device signer; the
+    input digest proves they are the bytes make_digests.py config1 built with
+    libsodium.  Accept bits, status bytes and transaction ids must equal the
+    reference's digests (re-serialise + OpenSSL + libsodium per row,
+    SerializedTransaction.cpp:220-230) through the host API
+    (stl_tx_blob_verify_batch) and the device-resident one-call path
+    (stl_signed_blob_verify_batch_device), under each dedup choice."""
+    import ctypes
+    from stellard_amd import _native as N
+    torch = torch_cuda
+    with open(datasets.DIGESTS) as f:
+        want = json.load(f)["config1"]
+
+    def signer_pks(seeds):
+        z = torch.zeros((seeds.shape[0], 32), dtype=torch.uint8, device="cuda")
+        return stl.sign_batch_device(torch.from_numpy(np.ascontiguousarray(seeds)).cuda(), z)[0].cpu().numpy()
+    plan = datasets.config1_plan(signer_pks)
+    n = plan["n"]
+    msgs = torch.from_numpy(datasets.config1_signing_hashes(plan)).cuda()
+    _, sig = stl.sign_batch_device(torch.from_numpy(np.ascontiguousarray(plan["seeds"][plan["who"]])).cuda(), msgs)
+    buf, offs, lens = datasets.config1_finish(plan, sig.cpu().numpy())
+    assert datasets.config1_inputs_h16(buf, lens) == want["inputs_h16"], "device signer / construction differs"
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    # host API: blobs from host memory, PCIe included
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    st = np.zeros(n, np.uint8)
+    ids = np.zeros((n, 32), np.uint8)
+    B = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    o64, l32 = offs.astype(np.uint64), lens.astype(np.uint32)
+    N.check(N.load().stl_tx_blob_verify_batch(B(buf), B(o64), B(l32), n, B(bm), B(st), B(ids), 0),
+            "stl_tx_blob_verify_batch")
+    assert sha(bm) == want["bitmap_sha256"]
+    assert sha(st) == want["status_sha256"]
+    assert sha(ids) == want["ids_sha256"]
+    # device-resident one call, each dedup choice
+    d_buf = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(offs).cuda()
+    d_len = torch.from_numpy(lens).cuda()
+    for flags in (0, stl.DEDUP_KEYS, stl.NO_AUTO_DEDUP):
+        o = stl.signed_blob_verify_batch_device(d_buf, d_off, d_len, tx_ids=True, policy=flags)
+        torch.cuda.synchronize()
+        assert _digest(stl, o["words"], n) == want["bitmap_sha256"], flags
+        assert sha(o["status"].cpu().numpy()) == want["status_sha256"], flags
+        assert sha(o["tx_id"].cpu().numpy()) == want["ids_sha256"], flags
+    assert int(stl.words_to_bool(o["words"], n).sum()) == want["accepted"]

@@ -166,6 +166,39 @@ def test_c_shards_equal_python_mirror():
             assert _c_shard_bytes(lib, lens, r, g) == shard.shard_range_bytes(lens, r, g), (n, g, r)
 
 
+def test_byte_shards_snap_to_the_verify_step():
+    """verify time steps every shard.QUANTUM rows (one
+    main-kernel wave per SIMD), so a byte-balanced boundary within 1 % of a
+    rank's bytes of a multiple of it moves there: config 5's ledgers
+    (log-uniform 113 B - 4 KB rows) over 2, 4 and 8 ranks get exactly 2^20 / g
+    rows per rank, bytes within 1 % of the share; the C function equals the
+    mirror; a boundary far from any multiple keeps its byte balance."""
+    from stellard_amd import _native
+    lib = _native.load()
+    rng = np.random.default_rng(0x5A1)
+    q = shard.QUANTUM
+    for trial in range(3):
+        n = 1 << 20
+        lens = np.exp(rng.uniform(np.log(113), np.log(4096), n)).astype(np.uint32)
+        total = int(lens.sum())
+        for g in (2, 4, 8):
+            b = [shard.shard_range_bytes(lens, r, g) for r in range(g)]
+            assert [hi - lo for lo, hi in b] == [n // g] * g, (trial, g)
+            per = [int(lens[lo:hi].sum()) for lo, hi in b]
+            assert max(abs(p - total / g) for p in per) <= 0.02 * total / g
+            for r in range(g):
+                assert _c_shard_bytes(lib, lens, r, g) == b[r], (trial, g, r)
+        # 3 ranks: boundaries near 349,525 rows, far from any multiple of q
+        b = [shard.shard_range_bytes(lens, r, 3) for r in range(3)]
+        assert all(lo % q for lo, _ in b[1:])
+        assert [_c_shard_bytes(lib, lens, r, 3) for r in range(3)] == b
+    # a heavy head: the snap would move too many bytes, so it stays put
+    lens = np.full(1 << 18, 200, np.uint32)
+    lens[: 1 << 16] = 4000
+    b = [shard.shard_range_bytes(lens, r, 2) for r in range(2)]
+    assert b[0][1] % q != 0 and [_c_shard_bytes(lib, lens, r, 2) for r in range(2)] == b
+
+
 def test_byte_shards_cover_align_and_balance():
     rng = np.random.default_rng(6)
     lens = np.exp(rng.uniform(np.log(100), np.log(4096), 200000)).astype(np.uint32)

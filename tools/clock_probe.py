@@ -45,6 +45,13 @@ def main():
                        "ses": sorted(set(se.tolist())),
                        "first_cycles": int(t.min()), "first_realtime": int(rt.min())}
     out["idle_2048"] = per
+    cu = {}
+    for t, rt, x, hw in a.tolist():
+        cu.setdefault((int(x) & 0xF, (int(hw) >> 8) & 0xFF), []).append((t, rt))
+    spans = [max(v[0] for v in vs) - min(v[0] for v in vs) for vs in cu.values() if len(vs) > 1]
+    rts = [max(v[1] for v in vs) - min(v[1] for v in vs) for vs in cu.values() if len(vs) > 1]
+    out["idle_2048_per_cu"] = {"cus": len(cu), "max_cycle_span_within_cu": max(spans) if spans else None,
+                               "max_realtime_span_within_cu_10ns": max(rts) if rts else None}
     n = 1 << 20
     rng = np.random.default_rng(1)
     seeds = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
@@ -62,15 +69,15 @@ def main():
         st1 = V.clock_stamp(nwg, s)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        ghz, per = V.clock_ghz(st0, st1)
-        out[f"loaded_{nwg}"] = {"ghz": ghz, "per_xcc": per, "ms_per_launch": dt * 1e3 / k,
+        ghz, per, ncu = V.clock_ghz(st0, st1)
+        out[f"loaded_{nwg}"] = {"ghz": ghz, "per_xcc": per, "cus_matched": ncu, "ms_per_launch": dt * 1e3 / k,
                                 "cycles_per_verify": (dt / k) * ghz * 1e9 / n if ghz else None}
     st0 = V.clock_stamp(256, s)
     torch.cuda.synchronize()
     time.sleep(0.05)
     st1 = V.clock_stamp(256, s)
     torch.cuda.synchronize()
-    out["idle_gap"] = dict(zip(("ghz", "per_xcc"), V.clock_ghz(st0, st1)))
+    out["idle_gap"] = dict(zip(("ghz", "per_xcc", "cus_matched"), V.clock_ghz(st0, st1)))
     print(json.dumps(out))
 
 
