@@ -339,7 +339,12 @@ int stl_bitmap_gatherv_device(const uint64_t *d_words, size_t nwords, uint64_t *
 void stl_shard_range(size_t n, int r, int g, size_t *lo, size_t *hi);
 /* Byte-balanced shard for variable-length rows (config 5: preimages or blobs
  * of 100 B - 4 KB): boundaries at the 64-aligned row where the prefix sum of
- * len crosses r/g of the total. */
+ * len crosses r/g of the total -- each then moved to the nearest multiple of
+ * the verify step (one main-kernel wave per SIMD of the first device: 65,536
+ * rows on 256 CUs; 65,536 before stl_init) when that moves its byte prefix by
+ * at most 2.5 % of one rank's share: the device-resident verify's time rises
+ * in steps of that many rows, so a shard just past a step would pay a whole
+ * extra step (config 5's 2^20 rows over 2, 4, 8 ranks: exactly 2^20 / g each). */
 void stl_shard_range_bytes(const uint32_t *len, size_t n, int r, int g, size_t *lo, size_t *hi);
 
 /* ---- request aggregator ----

@@ -853,11 +853,12 @@ void shard(size_t n, int r, int g, size_t* lo, size_t* hi) {
 // Byte-balanced 64-aligned shard boundaries: bound[r] = the 64-aligned row at
 // or after the first row whose byte prefix sum reaches r/g of the total --
 // then moved to the nearest multiple of g_shard_quantum rows when that moves
-// its byte prefix by at most 1 % of one rank's share (config 5's
-// 2^20-row ledger over 8 ranks byte-balances to 130,304-131,584 rows, and the
-// ranks past 131,072 paid a sliver of a second round; equal rows cost the
-// ranks at most 0.6 % of bytes, i.e. of the ~20 % of a rank's time that is
-// hashing).  tests/test_multigpu_host.py holds the Python mirror to it.
+// its byte prefix by at most 2.5 % of one rank's share (config
+// 5's 2^20-row ledger over 8 ranks byte-balances to 130,304-131,584 rows, and
+// the ranks past 131,072 paid a sliver of a second round: max / mean rank time
+// 1.03-1.11; equal rows cost a rank at most ~0.6 % of its bytes, i.e. of the
+// fifth of its time that is hashing).  tests/test_multigpu_host.py holds the
+// Python mirror to it.
 void shard_bytes_bounds(const uint32_t* len, size_t n, int g, std::vector<size_t>& bound) {
   bound.assign(g + 1, n);
   bound[0] = 0;
@@ -884,7 +885,7 @@ void shard_bytes_bounds(const uint32_t* len, size_t n, int g, std::vector<size_t
       const size_t c = (b - down <= up - b || up > n) ? down : up;
       const uint64_t pc = prefix(c);
       const uint64_t dev = pc > target ? pc - target : target - pc;
-      if (c > 0 && c < n && (__uint128_t)dev * (unsigned)g * 100u <= (__uint128_t)total) b = c;
+      if (c > 0 && c < n && (__uint128_t)dev * (unsigned)g * 40u <= (__uint128_t)total) b = c;
     }
     bound[r] = std::max(bound[r - 1], b);
   }

@@ -28,7 +28,7 @@ def shard_range_bytes(lens, rank, world, quantum=QUANTUM):
     stl_shard_range_bytes): boundary r is the 64-aligned row at or after the
     first row where the byte prefix sum reaches r/world of the total, moved to
     the nearest multiple of ``quantum`` rows when that moves its byte prefix by
-    at most 1 % of one rank's share.  Variable-length rows (config 5: 100 B -
+    at most 2.5 % of one rank's share.  Variable-length rows (config 5: 100 B -
     4 KB preimages) cost in proportion to their SHA-512 blocks, so ranks get
     equal bytes, not equal counts -- but the verify time rises in steps of
     ``quantum`` rows, so a shard just past a step is pulled back to it."""
@@ -51,7 +51,7 @@ def shard_range_bytes(lens, rank, world, quantum=QUANTUM):
             down = b // q * q
             up = down + q
             c = down if (b - down <= up - b or up > n) else up
-            if 0 < c < n and abs(int(csum[c]) - target) * world * 100 <= total:
+            if 0 < c < n and abs(int(csum[c]) - target) * world * 40 <= total:
                 b = c
         return b
 
