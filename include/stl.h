@@ -454,6 +454,10 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
                                         of more than this many SHA-512 blocks are hashed one per wave
                                         (schedules expanded side by side, rounds reading them from
                                         LDS): the longest row sets a small ledger's hash latency */
+#define STL_TUNE_SHARED_KEYS 9       /* 0 / 1 (default 1): with STL_DEDUP_KEYS (or the automatic choice) a
+                                        device-resident call of several chunks builds ONE key table for
+                                        all of them (the first chunk builds it, the others wait for it),
+                                        instead of one per chunk */
 #define STL_TUNE_RCCL_TIMEOUT_MS 7 /* 1..3,600,000 (default 120,000; env STL_RCCL_TIMEOUT_S): deadline of
                                       stl_comm_init_rank and stl_comm_sync */
 int stl_debug_tuning(int key, int value);

@@ -278,6 +278,7 @@ std::atomic<int> g_tune_sub_log2{0};  // log2 signatures per stream chunk; 0 = b
 std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even for one shard
 std::atomic<int> g_tune_quad{3};      // smallest chunks' main kernel on lane groups: bit 0 quads, bit 1 duos
 std::atomic<int> g_tune_long_hash{8}; // small batches: rows of more than this many blocks hashed one per wave (0 off)
+std::atomic<int> g_tune_shared_keys{1}; // key dedup over several chunks: one key domain per call (0: one per chunk)
 
 // Rows per step of verify time: the device-resident verify runs a chunk's
 // 64-signature units on its resident waves, two per SIMD, so its time rises in
@@ -347,6 +348,8 @@ struct StreamCtx {
   // over pool streams
   hipEvent_t fork = nullptr;
   hipEvent_t join[stl::kMaxVerifyStreams] = {};
+  // a launch's shared key domain is built (stl::VerifyExec::key_ready)
+  hipEvent_t keys = nullptr;
   // device-resident automatic dedup: host-mapped word the key sample kernel
   // writes after each call on this stream (1 = its keys repeated); the next
   // call reads it without waiting (feedback, so a stale value only picks the
@@ -368,16 +371,19 @@ struct StreamCtx {
     }
     if (fork) (void)hipEventDestroy(fork);
     fork = nullptr;
+    if (keys) (void)hipEventDestroy(keys);
+    keys = nullptr;
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
   }
-  bool holds_memory() const { return auto_flag || scratch.p || ws.p || queue.p || fork || done; }
+  bool holds_memory() const { return auto_flag || scratch.p || ws.p || queue.p || fork || keys || done; }
   // moves every buffer and event of `o` into this (empty) context
   void adopt(StreamCtx& o) {
     std::swap(ws, o.ws);
     std::swap(queue, o.queue);
     std::swap(scratch, o.scratch);
     std::swap(fork, o.fork);
+    std::swap(keys, o.keys);
     for (uint32_t j = 0; j < stl::kMaxVerifyStreams; ++j) std::swap(join[j], o.join[j]);
     std::swap(auto_flag, o.auto_flag);
     std::swap(auto_flag_dev, o.auto_flag_dev);
@@ -809,6 +815,10 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   }
   if (S > 1 && !c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
   x.fork = c.fork;
+  if (S > 1 && dedup && g_tune_shared_keys.load()) {  // the chunks share one key domain in the caller's workspace
+    if (!c.keys) STL_TRY(hipEventCreateWithFlags(&c.keys, hipEventDisableTiming));
+    x.key_ready = c.keys;
+  }
   if (fault_now() || stl::launch_verify(sig, msg_or_k, pk, (uint32_t)n, words, mode, pre_k, x) != hipSuccess) {
     for (uint32_t j = 1; j < S; ++j) (void)hipStreamSynchronize(pool[j]);
     return STL_EHIP;
@@ -1485,6 +1495,9 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_LONG_HASH:
       if (value < 0 || value > 62) return STL_EINVAL;
       return g_tune_long_hash.exchange(value);
+    case STL_TUNE_SHARED_KEYS:
+      if (value != 0 && value != 1) return STL_EINVAL;
+      return g_tune_shared_keys.exchange(value);
     default:
       return STL_EINVAL;
   }
@@ -1822,6 +1835,9 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   uint8_t* pk = blob ? msg + 96 * n : const_cast<uint8_t*>(pk_in);
   uint8_t* st = status;
   for (uint32_t j = 0; j < S; ++j) STL_RC(kc[j]->ws.ensure(stl::verify_ws_bytes(d.grid, dedup)));
+  // dedup over several chunks: one key domain for the call (VerifyExec::key_ws)
+  const bool shared_keys = dedup && S > 1 && n <= stl::kPreChunk && sub > pair_max(d) && g_tune_shared_keys.load();
+  if (shared_keys && !c.keys) STL_TRY(hipEventCreateWithFlags(&c.keys, hipEventDisableTiming));
   if (S > 1 || ahead) {
     if (!c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
     if (!c.join[1]) STL_TRY(hipEventCreateWithFlags(&c.join[1], hipEventDisableTiming));
@@ -1874,6 +1890,17 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     if (S > 1 && k == 2 && hipStreamWaitEvent(ks[0], c.join[2], 0) != hipSuccess) return fail(STL_EHIP);
     stl::VerifyExec x = exec_for(cnt, j);
     x.points_done = ahead;
+    if (shared_keys) {
+      // one key domain for the whole call, in the caller's workspace: built by
+      // chunk 0 on the caller's stream after its scalar kernel -- for blobs
+      // once the other rows' keys are out of the pass on pool stream 1
+      x.key_ws = static_cast<uint4*>(kc[0]->ws.p);
+      x.key_n = (uint32_t)n;
+      x.key_base = (uint32_t)b0;
+      x.key_build = k == 0;
+      x.key_ready = c.keys;
+      x.key_after = blob ? c.join[2] : nullptr;
+    }
     if (fault_now() || stl::launch_verify(sig + 64 * b0, msg + 32 * b0, pk + 32 * b0, cnt, words + b0 / 64, mode,
                                           false, x) != hipSuccess)
       return fail(STL_EHIP);

@@ -101,6 +101,21 @@ struct VerifyExec {
   uint32_t duo_max = 0;                 // up to this size on four (verify_main_group_kernel<2>); 0: never
   bool points_done = false;             // one lane-pair chunk whose point role already ran
                                         // (launch_verify_points, ordered before this launch)
+  // Key dedup over a whole batch (kModeDedupKeys): one key domain -- hash
+  // slots, owners, decoded keys, key tables -- for every chunk, instead of one
+  // per chunk (round 6: a chunk of config 1's 100k rows rebuilt the same 1,000
+  // keys' tables on the critical path).  launch_verify sets it up by itself
+  // for a launch of several chunks when key_ready is given; a caller that
+  // runs the chunks as separate launches (the one-call checkSign) sets
+  // key_ws to the workspace holding the domain, key_n to its rows, key_base to
+  // this launch's first row in it, and key_build on the launch that builds it
+  // (its first chunk's stream records key_ready; the others wait for it).
+  hipEvent_t key_ready = nullptr;
+  hipEvent_t key_after = nullptr;       // the builder's stream waits for it first (keys of other rows
+                                        // still being produced, e.g. by the blob pass on another stream)
+  uint4* key_ws = nullptr;
+  uint32_t key_base = 0, key_n = 0;
+  bool key_build = false;
 };
 // Whether launch_verify of n <= kPreChunk signatures (one chunk) runs its
 // phase 1 as the two-role lane-pair kernel -- then its point role (the two

@@ -590,7 +590,8 @@ __global__ __launch_bounds__(kBlock) void key_table_wide_kernel(const uint32_t* 
 __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
     const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk, uint32_t base, uint32_t cnt, uint32_t policy,
     uint4* __restrict__ pre, uint64_t* __restrict__ fb_words, const uint32_t* __restrict__ rep,
-    const uint32_t* __restrict__ uid_of, const uint4* __restrict__ keytab, const uint32_t* __restrict__ counter) {
+    const uint32_t* __restrict__ uid_of, const uint4* __restrict__ keytab, const uint32_t* __restrict__ counter,
+    uint32_t kcnt) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   const bool live = t < cnt;
   const uint32_t tt = live ? t : cnt - 1;
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   h.pad = uid;
   const uint32_t nu = *counter;
   if (nu <= kKeyTables) h.tops |= kHalfKeyed | c_neg;  // the main kernel reads the key's table
-  if (wide_keys(nu, cnt)) h.tops |= kHalfKeyedWide;
+  if (wide_keys(nu, kcnt)) h.tops |= kHalfKeyedWide;  // kcnt: the key domain's rows (key_table_wide_kernel's choice)
   if (live) {
     q[4] = make_uint4(w[16], w[17], w[18], w[19]);
     st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
@@ -1846,6 +1847,49 @@ hipError_t launch_verify_points(const uint8_t* sig, const uint8_t* pk, uint32_t 
   return hipGetLastError();
 }
 
+// The key-dedup area of a verify workspace (after verify_ws_bytes(grid)):
+// hash slots, per-row representative, per-owner id and owner row, the
+// distinct-key counter, the decoded keys and the shared / wide key tables.
+struct KeyDomain {
+  uint32_t *kslots, *rep, *uid_of, *owners, *counter;
+  uint4 *keytab, *keytabs, *widetabs;
+};
+static KeyDomain key_domain(uint4* ws, uint32_t grid) {
+  KeyDomain k;
+  uint32_t* dd = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws) + verify_ws_bytes(grid));
+  k.kslots = dd;
+  k.rep = k.kslots + kDedupSlots;
+  k.uid_of = k.rep + kPreChunk;
+  k.owners = k.uid_of + kPreChunk;
+  k.counter = k.owners + kPreChunk;
+  k.keytab = reinterpret_cast<uint4*>(k.counter + 64);
+  k.keytabs = k.keytab + (size_t)kPreChunk * 5;
+  k.widetabs = k.keytabs + (size_t)kKeyTables * kTableQuadsPerKey;
+  return k;
+}
+
+// The dedup chain over rows [base, base+cnt) (cnt <= kPreChunk): hash slots,
+// owners, decoded keys, shared or wide key tables -- rep[i] for row base+i.
+static hipError_t launch_key_domain(const uint8_t* pk, uint32_t base, uint32_t cnt, const KeyDomain& kd,
+                                    hipStream_t stream) {
+  const dim3 g1((cnt + kBlock - 1) / kBlock);
+  uint32_t nslots = 64;
+  while (nslots < 2 * cnt) nslots <<= 1;  // <= kDedupSlots
+  hipError_t e = hipMemsetAsync(kd.kslots, 0xff, (size_t)nslots * 4, stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(kd.counter, 0, 4, stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(key_insert_kernel, g1, dim3(kBlock), 0, stream, pk, base, cnt, kd.kslots, nslots - 1, kd.rep,
+                     kd.uid_of, kd.counter, kd.owners);
+  hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, kd.counter, kd.owners, kd.keytab,
+                     kd.keytabs, cnt);
+  const uint32_t wmax = cnt / kWideKeyRepeat < kWideKeys ? cnt / kWideKeyRepeat : kWideKeys;  // keys that can be wide
+  if (wmax > 0)
+    hipLaunchKernelGGL(key_table_wide_kernel, dim3((wmax * (uint32_t)kWideKeyEntries + kBlock - 1) / kBlock),
+                       dim3(kBlock), 0, stream, kd.counter, cnt, kd.keytab, kd.widetabs);
+  return hipGetLastError();
+}
+
 // One chunk (<= kPreChunk signatures at [base, base+cnt)) on one stream and
 // workspace: phase 1, main, fallback.  `qctr` is the chunk's zeroed counter
 // of the main kernel's unit queue.
@@ -1864,15 +1908,18 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
   uint4* pre = ws + (size_t)grid * (kWsBytesPerBlock / 16);
   uint64_t* fb = reinterpret_cast<uint64_t*>(pre + (size_t)kPreChunk * 14);
   const bool dedup = (policy & kModeDedupKeys) != 0;
-  uint32_t* dd = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws) + verify_ws_bytes(grid));
-  uint32_t* kslots = dd;
-  uint32_t* rep = kslots + kDedupSlots;
-  uint32_t* uid_of = rep + kPreChunk;
-  uint32_t* owners = uid_of + kPreChunk;
-  uint32_t* counter = owners + kPreChunk;
-  uint4* keytab = reinterpret_cast<uint4*>(counter + 64);
-  uint4* keytabs = keytab + (size_t)kPreChunk * 5;
-  uint4* widetabs = keytabs + (size_t)kKeyTables * kTableQuadsPerKey;
+  // a launch-wide key domain (KeyDomain: one key table for every chunk of
+  // the launch, in x.key_ws) or this chunk's own, in its workspace
+  const KeyDomain kd = key_domain(x.key_ws ? x.key_ws : ws, grid);
+  uint32_t* kslots = kd.kslots;
+  uint32_t* rep = x.key_ws ? kd.rep + x.key_base + base : kd.rep;
+  uint32_t* uid_of = kd.uid_of;
+  uint32_t* owners = kd.owners;
+  uint32_t* counter = kd.counter;
+  uint4* keytab = kd.keytab;
+  uint4* keytabs = kd.keytabs;
+  uint4* widetabs = kd.widetabs;
+  const uint32_t kcnt = x.key_ws ? x.key_n : cnt;  // rows of the key domain (the wide-table choice)
   {
     const dim3 g1((cnt + kBlock - 1) / kBlock);
     const uint32_t units = (cnt + 63) / 64;
@@ -1914,22 +1961,22 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
     } else if (fused) {
       // phase 1 done
     } else if (dedup) {
-      uint32_t nslots = 64;
-      while (nslots < 2 * cnt) nslots <<= 1;  // <= kDedupSlots
-      hipError_t e = hipMemsetAsync(kslots, 0xff, (size_t)nslots * 4, stream);
-      if (e != hipSuccess) return e;
-      e = hipMemsetAsync(counter, 0, 4, stream);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(key_insert_kernel, g1, dim3(kBlock), 0, stream, pk, base, cnt, kslots, nslots - 1, rep, uid_of,
-                         counter, owners);
-      hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, counter, owners, keytab, keytabs,
-                         cnt);
-      const uint32_t wmax = cnt / kWideKeyRepeat < kWideKeys ? cnt / kWideKeyRepeat : kWideKeys;  // keys that can be wide
-      if (wmax > 0)
-        hipLaunchKernelGGL(key_table_wide_kernel, dim3((wmax * (uint32_t)kWideKeyEntries + kBlock - 1) / kBlock),
-                           dim3(kBlock), 0, stream, counter, cnt, keytab, widetabs);
+      if (!x.key_ws) {
+        hipError_t e = launch_key_domain(pk, base, cnt, kd, stream);
+        if (e != hipSuccess) return e;
+      } else if (x.key_build) {
+        // the launch-wide domain, built once on this (the first) stream
+        // after this chunk's scalar kernel, over every row of the launch
+        hipError_t e = x.key_after ? hipStreamWaitEvent(stream, x.key_after, 0) : hipSuccess;
+        if (e == hipSuccess) e = launch_key_domain(pk, 0, x.key_n, kd, stream);
+        if (e == hipSuccess) e = hipEventRecord(x.key_ready, stream);
+        if (e != hipSuccess) return e;
+      } else {
+        hipError_t e = hipStreamWaitEvent(stream, x.key_ready, 0);
+        if (e != hipSuccess) return e;
+      }
       hipLaunchKernelGGL(verify_point_kernel_keyed, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb,
-                         rep, uid_of, keytab, counter);
+                         rep, uid_of, keytab, counter, kcnt);
     } else {
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }
@@ -2002,12 +2049,23 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
       if (e != hipSuccess) return e;
     }
   }
+  // one key domain for every chunk of the launch (see VerifyExec::key_ready):
+  // built by chunk 0 on streams[0] right after its scalar kernel
+  VerifyExec xk = x;
+  const bool shared_keys = (policy & kModeDedupKeys) && nchunks > 1 && n <= kPreChunk && x.key_ready &&
+                           !x.key_ws && csize > x.pair_max;  // chunk 0 runs the one-lane path that builds it
+  if (shared_keys) {
+    xk.key_ws = x.ws[0];
+    xk.key_base = 0;
+    xk.key_n = n;
+  }
   for (uint64_t c = 0; c < nchunks; ++c) {  // 64-bit: n may reach 2^32 - 64
     const uint32_t j = (uint32_t)(c % S);
     const uint32_t base = (uint32_t)(c * csize);
     const uint32_t cnt = n - base < csize ? n - base : csize;
     uint32_t* q = x.main_queue ? queue_counters(x.ws[j], x.grid) + c / S : nullptr;
-    e = verify_chunk(sig, msg_or_k, pk, base, cnt, bitmap, policy, pre_k, x, x.streams[j], x.ws[j], q,
+    if (shared_keys) xk.key_build = c == 0;
+    e = verify_chunk(sig, msg_or_k, pk, base, cnt, bitmap, policy, pre_k, xk, x.streams[j], x.ws[j], q,
                      S > 1 ? nullptr : x.clock);
     if (e != hipSuccess) return e;
   }

@@ -603,6 +603,7 @@ TUNE_QUAD = N.STL_TUNE_QUAD
 TUNE_STREAM_WORKSPACES = N.STL_TUNE_STREAM_WORKSPACES
 TUNE_RCCL_TIMEOUT_MS = N.STL_TUNE_RCCL_TIMEOUT_MS
 TUNE_LONG_HASH = N.STL_TUNE_LONG_HASH
+TUNE_SHARED_KEYS = N.STL_TUNE_SHARED_KEYS
 
 
 def debug_tuning(key, value):
@@ -676,7 +677,8 @@ def execution_settings():
     lib = N.load()
     return {name: lib.stl_debug_tuning(key, -1) for name, key in (
         ("fused_prep", TUNE_FUSED_PREP), ("main_queue", TUNE_MAIN_QUEUE), ("streams", TUNE_STREAMS),
-        ("chunk_log2", TUNE_CHUNK_LOG2), ("quad", TUNE_QUAD), ("long_hash", TUNE_LONG_HASH))}
+        ("chunk_log2", TUNE_CHUNK_LOG2), ("quad", TUNE_QUAD), ("long_hash", TUNE_LONG_HASH),
+        ("shared_keys", TUNE_SHARED_KEYS))}
 
 
 def sign_batch_device(seed, msg, stream=None):

@@ -561,6 +561,71 @@ def test_batcher_verdicts(stl, oracle, golden):
         assert s["completed"] == len(sig) + len(blobs)
 
 
+@pytest.mark.parametrize("policy", [0, 1])
+def test_shared_key_domain_same_bits(stl, golden, oracle, torch_cuda, policy):
+    """Round 6: a device-resident call of several chunks with key dedup builds
+    ONE key domain for all of them (STL_TUNE_SHARED_KEYS, default on): its
+    first chunk builds the hash slots, decoded keys and wide / shared key
+    tables over every row, the others wait for them.  Bits equal the
+    per-chunk domains' and the no-dedup path's, at sizes of 2 chunks (100k,
+    300k), 4 chunks (1M) and with wide (1,000 signers) and 9-entry (10,000
+    signers on 100k rows: < 32 rows per key) tables, 5 % of rows mutated --
+    and through the one-call checkSign from preimages."""
+    torch = torch_cuda
+    rng = np.random.default_rng(0x5EED5)
+    for n, signers in ((100_000, 1000), (300_000, 1000), (1 << 20, 1000), (100_000, 10_000)):
+        aseed = rng.integers(0, 256, (signers, 32), dtype=np.uint8)
+        who = rng.integers(0, signers, n)
+        msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).cuda()
+        pkd, sigd = stl.sign_batch_device(torch.from_numpy(aseed[who]).cuda(), msgs)
+        bad = rng.random(n) < 0.05
+        col = torch.from_numpy(rng.integers(0, 64, int(bad.sum()))).cuda()
+        sigd[torch.from_numpy(np.nonzero(bad)[0]).cuda(), col] ^= 0x10
+        got = {}
+        for shared in (1, 0):
+            old = stl.debug_tuning(stl.TUNE_SHARED_KEYS, shared)
+            try:
+                w = stl.verify_batch_device(sigd, msgs, pkd, policy=policy | stl.DEDUP_KEYS)
+                torch.cuda.synchronize()
+                got[shared] = stl.words_to_bool(w, n)
+            finally:
+                stl.debug_tuning(stl.TUNE_SHARED_KEYS, old)
+        w = stl.verify_batch_device(sigd, msgs, pkd, policy=policy | stl.NO_AUTO_DEDUP)
+        torch.cuda.synchronize()
+        plain = stl.words_to_bool(w, n)
+        assert np.array_equal(got[1], got[0]), (n, signers)
+        assert np.array_equal(got[1], plain), (n, signers)
+        assert np.array_equal(plain, ~bad), (n, signers)
+        samp = rng.choice(n, 2000, replace=False)
+        s_np, m_np, p_np = sigd.cpu().numpy(), msgs.cpu().numpy(), pkd.cpu().numpy()
+        assert np.array_equal(got[1][samp], oracle.verify_batch(s_np[samp], m_np[samp], p_np[samp], policy=policy))
+    # one-call checkSign over preimages, 2 chunks, forced dedup, shared vs not
+    n = 150_000
+    lens = rng.integers(113, 1500, n).astype(np.int32)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum(lens[:-1])
+    pre = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 16, dtype=np.uint8)
+    d_pre = torch.from_numpy(pre).cuda()
+    d_off = torch.from_numpy(offs).cuda()
+    d_len = torch.from_numpy(lens).cuda()
+    m = stl.tx_hash_batch_device(d_pre, d_off, d_len)
+    aseed = rng.integers(0, 256, (500, 32), dtype=np.uint8)
+    pkd, sigd = stl.sign_batch_device(torch.from_numpy(aseed[rng.integers(0, 500, n)]).cuda(), m)
+    bad = rng.random(n) < 0.03
+    sigd[torch.from_numpy(np.nonzero(bad)[0]).cuda(), 50] ^= 0x04
+    outs = []
+    for shared in (1, 0):
+        old = stl.debug_tuning(stl.TUNE_SHARED_KEYS, shared)
+        try:
+            w = stl.tx_verify_batch_device(d_pre, d_off, d_len, sigd, pkd, policy=policy | stl.DEDUP_KEYS)
+            torch.cuda.synchronize()
+            outs.append(stl.words_to_bool(w, n))
+        finally:
+            stl.debug_tuning(stl.TUNE_SHARED_KEYS, old)
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], ~bad)
+
+
 @pytest.mark.parametrize("policy", [0, 1, 4])
 def test_dedup_keys_same_bits(stl, golden, oracle, torch_cuda, policy):
     """STL_DEDUP_KEYS (each distinct key decoded once per batch) gives the same
