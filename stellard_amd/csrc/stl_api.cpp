@@ -279,6 +279,7 @@ std::atomic<int> g_tune_byte_shards{0};  // test hook: byte-balanced shards even
 std::atomic<int> g_tune_quad{3};      // smallest chunks' main kernel on lane groups: bit 0 quads, bit 1 duos
 std::atomic<int> g_tune_long_hash{8}; // small batches: rows of more than this many blocks hashed one per wave (0 off)
 std::atomic<int> g_tune_shared_keys{1}; // key dedup over several chunks: one key domain per call (0: one per chunk)
+std::atomic<int> g_tune_wide_min{0};    // key domains of fewer rows build no wide key tables (the 9-entry ones)
 
 // Rows per step of verify time: the device-resident verify runs a chunk's
 // 64-signature units on its resident waves, two per SIMD, so its time rises in
@@ -348,8 +349,10 @@ struct StreamCtx {
   // over pool streams
   hipEvent_t fork = nullptr;
   hipEvent_t join[stl::kMaxVerifyStreams] = {};
-  // a launch's shared key domain is built (stl::VerifyExec::key_ready)
+  // a launch's shared key domain is built (stl::VerifyExec::key_ready); the
+  // one-call blob path's two parse kernels are done (the keys are out)
   hipEvent_t keys = nullptr;
+  hipEvent_t parsed[2] = {};
   // device-resident automatic dedup: host-mapped word the key sample kernel
   // writes after each call on this stream (1 = its keys repeated); the next
   // call reads it without waiting (feedback, so a stale value only picks the
@@ -373,10 +376,16 @@ struct StreamCtx {
     fork = nullptr;
     if (keys) (void)hipEventDestroy(keys);
     keys = nullptr;
+    for (hipEvent_t& e : parsed) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
   }
-  bool holds_memory() const { return auto_flag || scratch.p || ws.p || queue.p || fork || keys || done; }
+  bool holds_memory() const {
+    return auto_flag || scratch.p || ws.p || queue.p || fork || keys || parsed[0] || parsed[1] || done;
+  }
   // moves every buffer and event of `o` into this (empty) context
   void adopt(StreamCtx& o) {
     std::swap(ws, o.ws);
@@ -384,6 +393,8 @@ struct StreamCtx {
     std::swap(scratch, o.scratch);
     std::swap(fork, o.fork);
     std::swap(keys, o.keys);
+    std::swap(parsed[0], o.parsed[0]);
+    std::swap(parsed[1], o.parsed[1]);
     for (uint32_t j = 0; j < stl::kMaxVerifyStreams; ++j) std::swap(join[j], o.join[j]);
     std::swap(auto_flag, o.auto_flag);
     std::swap(auto_flag_dev, o.auto_flag_dev);
@@ -750,6 +761,18 @@ uint32_t duo_max(const Device& d) { return (g_tune_quad.load() & 2) ? d.grid * s
 unsigned long long* dev_counters(Device& d);
 const stl::PhaseClock* phase_clock(Device& d);
 
+// A pool kernel stream that a call running on streams[0..S) does not use:
+// the shared key domain is built there, beside the chunks' scalar kernels
+// (stl::VerifyExec::key_stream); nullptr when every one is taken.
+hipStream_t key_stream_for(const Device& d, const hipStream_t* used, uint32_t S) {
+  for (hipStream_t c : {d.stream, d.stream2}) {
+    bool taken = c == nullptr;
+    for (uint32_t j = 0; j < S; ++j) taken = taken || used[j] == c;
+    if (!taken) return c;
+  }
+  return nullptr;
+}
+
 // Plans and enqueues one launch_verify of n signatures on stream s: with
 // `streams` > 1 (device-resident API only: the host batch API already overlaps
 // its copies with the previous chunk's kernels) chunks also go to the pool
@@ -763,6 +786,7 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   const bool dedup = (mode & stl::kModeDedupKeys) != 0;
   stl::VerifyExec x;
   x.grid = verify_grid_for(d, n);
+  x.ws_grid = d.grid;  // every workspace is verify_ws_bytes(d.grid, ...)
   x.pair_max = pair_max(d);
   x.quad_max = quad_max(d);
   x.duo_max = duo_max(d);
@@ -815,12 +839,15 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   }
   if (S > 1 && !c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
   x.fork = c.fork;
+  x.wide_min = (uint32_t)g_tune_wide_min.load();
   if (S > 1 && dedup && g_tune_shared_keys.load()) {  // the chunks share one key domain in the caller's workspace
     if (!c.keys) STL_TRY(hipEventCreateWithFlags(&c.keys, hipEventDisableTiming));
     x.key_ready = c.keys;
+    x.key_stream = key_stream_for(d, pool, S);  // built beside the scalar kernels when a pool stream is idle
   }
   if (fault_now() || stl::launch_verify(sig, msg_or_k, pk, (uint32_t)n, words, mode, pre_k, x) != hipSuccess) {
     for (uint32_t j = 1; j < S; ++j) (void)hipStreamSynchronize(pool[j]);
+    if (x.key_stream) (void)hipStreamSynchronize(x.key_stream);
     return STL_EHIP;
   }
   return STL_OK;
@@ -1498,6 +1525,9 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_SHARED_KEYS:
       if (value != 0 && value != 1) return STL_EINVAL;
       return g_tune_shared_keys.exchange(value);
+    case STL_TUNE_WIDE_MIN_ROWS:
+      if (value < 0 || value > (int)stl::kPreChunk) return STL_EINVAL;
+      return g_tune_wide_min.exchange(value);
     default:
       return STL_EINVAL;
   }
@@ -1803,6 +1833,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   auto exec_for = [&](uint32_t cnt, uint32_t j) {
     stl::VerifyExec x;
     x.grid = verify_grid_for(d, cnt);
+    x.ws_grid = d.grid;  // every workspace is verify_ws_bytes(d.grid, ...)
     x.pair_max = pair_max(d);
     x.quad_max = quad_max(d);
     x.duo_max = duo_max(d);
@@ -1835,9 +1866,17 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   uint8_t* pk = blob ? msg + 96 * n : const_cast<uint8_t*>(pk_in);
   uint8_t* st = status;
   for (uint32_t j = 0; j < S; ++j) STL_RC(kc[j]->ws.ensure(stl::verify_ws_bytes(d.grid, dedup)));
-  // dedup over several chunks: one key domain for the call (VerifyExec::key_ws)
+  // dedup over several chunks: one key domain for the call (VerifyExec::key_ws),
+  // built on an idle pool stream (cs) as soon as the keys are known -- at
+  // once for preimages, after both parse kernels for blobs -- beside the
+  // hashing and the scalar kernels; with no idle stream, by chunk 0 after its
+  // scalar kernel
   const bool shared_keys = dedup && S > 1 && n <= stl::kPreChunk && sub > pair_max(d) && g_tune_shared_keys.load();
+  hipStream_t cs = shared_keys ? key_stream_for(d, ks, S) : nullptr;
   if (shared_keys && !c.keys) STL_TRY(hipEventCreateWithFlags(&c.keys, hipEventDisableTiming));
+  if (cs && blob)
+    for (hipEvent_t& e : c.parsed)
+      if (!e) STL_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (S > 1 || ahead) {
     if (!c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
     if (!c.join[1]) STL_TRY(hipEventCreateWithFlags(&c.join[1], hipEventDisableTiming));
@@ -1847,6 +1886,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   }
   auto fail = [&](int rc) {
     if (S > 1 || ahead) (void)hipStreamSynchronize(ks[1]);
+    if (cs) (void)hipStreamSynchronize(cs);
     return rc;
   };
   if (ahead) {
@@ -1864,7 +1904,8 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     hipError_t e;
     if (blob)
       e = stl::launch_tx_blob(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, sig + 64 * b0, pk + 32 * b0,
-                              id ? id + 32 * b0 : nullptr, st + b0, qw, hash_grid(d), js, kind);
+                              id ? id + 32 * b0 : nullptr, st + b0, qw, hash_grid(d), js, kind,
+                              cs ? c.parsed[js == ks[0] ? 0 : 1] : nullptr);
     else
       e = stl::launch_tx_hash(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, qw, hash_grid(d), js,
                               hash_long_min(d, n));
@@ -1879,6 +1920,21 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     if (!rc) rc = hash(sub, n - sub, ks[1], q[1]);
     if (!rc && hipEventRecord(c.join[2], ks[1]) != hipSuccess) rc = STL_EHIP;
     if (rc) return fail(rc);
+  }
+  if (cs) {  // the call's key domain on its own stream, in the caller's workspace
+    hipError_t e = hipSuccess;
+    if (blob) {
+      e = hipStreamWaitEvent(cs, c.parsed[0], 0);
+      if (e == hipSuccess) e = hipStreamWaitEvent(cs, c.parsed[1], 0);
+    } else {
+      e = hipStreamWaitEvent(cs, c.fork, 0);
+    }
+    if (e == hipSuccess && fault_now()) e = hipErrorUnknown;
+    if (e == hipSuccess)
+      e = stl::launch_key_domain_ws(pk, (uint32_t)n, static_cast<uint4*>(kc[0]->ws.p), d.grid,
+                                    (uint32_t)g_tune_wide_min.load(), cs);
+    if (e == hipSuccess) e = hipEventRecord(c.keys, cs);
+    if (e != hipSuccess) return fail(STL_EHIP);
   }
   size_t k = 0;
   for (size_t b0 = 0; b0 < n; b0 += sub, ++k) {
@@ -1897,10 +1953,11 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
       x.key_ws = static_cast<uint4*>(kc[0]->ws.p);
       x.key_n = (uint32_t)n;
       x.key_base = (uint32_t)b0;
-      x.key_build = k == 0;
+      x.key_build = k == 0 && !cs;
       x.key_ready = c.keys;
-      x.key_after = blob ? c.join[2] : nullptr;
+      x.key_after = blob && !cs ? c.join[2] : nullptr;
     }
+    x.wide_min = (uint32_t)g_tune_wide_min.load();
     if (fault_now() || stl::launch_verify(sig + 64 * b0, msg + 32 * b0, pk + 32 * b0, cnt, words + b0 / 64, mode,
                                           false, x) != hipSuccess)
       return fail(STL_EHIP);

@@ -82,6 +82,8 @@ struct PhaseClock {
 constexpr uint32_t kMaxVerifyStreams = 4;
 struct VerifyExec {
   uint32_t grid = 1;                    // resident workgroups = per-lane workspace slots per ws
+  uint32_t ws_grid = 0;                 // the grid the workspaces were sized for (verify_ws_bytes): the key
+                                        // domain sits after it, wherever a launch's own grid ends (0: grid)
   uint32_t pair_max = 0;                // chunks up to this size run two lanes per signature
   const uint4* wide = nullptr;          // wide base tables
   unsigned long long* counters = nullptr;
@@ -116,7 +118,21 @@ struct VerifyExec {
   uint4* key_ws = nullptr;
   uint32_t key_base = 0, key_n = 0;
   bool key_build = false;
+  // launch_verify's own shared domain: built on this otherwise idle stream
+  // (forked from streams[0]) beside the chunks' scalar kernels, every chunk
+  // waiting for key_ready; nullptr: built by chunk 0 after its scalar kernel
+  hipStream_t key_stream = nullptr;
+  // rows below which a key domain builds no wide (137-entry) key tables --
+  // the 9-entry ones instead -- so a short call does not wait for the wide
+  // build (STL_TUNE_WIDE_MIN_ROWS)
+  uint32_t wide_min = 0;
 };
+// The dedup chain over rows [0, n) of pk into the key domain of workspace ws
+// (grid: its resident workgroups) on `stream` -- what a chunk with
+// kModeDedupKeys builds for itself, for a caller that runs it beside other
+// work and hands the domain to the chunks through VerifyExec::key_ws.
+hipError_t launch_key_domain_ws(const uint8_t* pk, uint32_t n, uint4* ws, uint32_t grid, uint32_t wide_min,
+                                hipStream_t stream);
 // Whether launch_verify of n <= kPreChunk signatures (one chunk) runs its
 // phase 1 as the two-role lane-pair kernel -- then its point role (the two
 // square-root chains; needs only the signatures and keys) may be launched
@@ -147,9 +163,11 @@ inline size_t blob_queue_bytes(size_t n) { return blob_side_offset(n) + 128 * n;
 hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint32_t* qws, uint32_t grid, hipStream_t stream, uint32_t long_min = 0);
 // qws: blob_queue_bytes(n)
+// parsed (nullable): recorded after the parse kernel (the rows' signatures and
+// keys are out; the hashing follows)
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
-                          hipStream_t stream, uint32_t kind = 0u /* STL_BLOB_* */);
+                          hipStream_t stream, uint32_t kind = 0u /* STL_BLOB_* */, hipEvent_t parsed = nullptr);
 // Wide base tables (stl_verify_core.h): 2 * 32769 rows of 28 words.
 constexpr size_t kWideTableBytes = 2ull * 32769 * 28 * 4;
 // Key-repeat sample of [0, n): *flag = 1 when a quarter of up to 2,048 sampled

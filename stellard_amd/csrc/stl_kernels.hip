@@ -370,9 +370,11 @@ __global__ __launch_bounds__(kBlock) void verify_finish_pair_kernel(uint32_t cnt
 //                       work per lane stays bounded;
 //   key_decode_kernel   one lane per distinct key: the square-root chain of -A,
 //                       and the key's 9-entry table;
-//   key_table_wide_kernel  few keys, many signatures each (kWideKeys,
-//                       kWideKeyRepeat): one lane per (key, j), j*(-A) for
-//                       j = 0..136, the table of c's radix-256 digit pairs;
+//   key_table_wide_base_kernel / key_table_wide_pair_kernel  few keys, many
+//                       signatures each (kWideKeys, kWideKeyRepeat): j*(-A)
+//                       for j = 0..136, the table of c's radix-256 digit
+//                       pairs -- 24 entries by double-and-add, the others one
+//                       addition of two of them;
 //   verify_point_kernel_keyed  the point half with only R decoded.
 constexpr uint32_t kKeyEmpty = 0xffffffffu;
 constexpr int kKeyProbes = 32;
@@ -539,17 +541,11 @@ __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __
   }
 }
 
-// One lane per (key u, multiple j): j*(-A) by double-and-add over j's 8 bits
-// from the decoded key, stored in cached form (a table row as
-// build_cached_table writes it).  Exits unless the chunk is in wide mode.
-__global__ __launch_bounds__(kBlock) void key_table_wide_kernel(const uint32_t* __restrict__ counter, uint32_t cnt,
-                                                                const uint4* __restrict__ keytab,
-                                                                uint4* __restrict__ widetabs) {
-  const uint32_t nu = *counter;
-  if (!wide_keys(nu, cnt)) return;
-  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t u = g / (uint32_t)kWideKeyEntries, j = g % (uint32_t)kWideKeyEntries;
-  if (u >= nu) return;  // no wave-level collective in this kernel
+// The chunk's wide key tables j*(-A), j = 0..136, in two stages
+// (stl_verify_core.h wide_base_index / wide_pair_entry), each a no-op unless
+// the chunk is in wide mode.  Stage 1: one lane per (key u, i < 24) builds
+// entry wide_base_index(i) by double-and-add from the decoded key.
+__device__ __forceinline__ void wide_key_point(fe& x, fe& y, const uint4* __restrict__ keytab, uint32_t u) {
   const uint4* kq = keytab + (size_t)u * 5;
   uint32_t kw[20];
 #pragma unroll
@@ -557,32 +553,44 @@ __global__ __launch_bounds__(kBlock) void key_table_wide_kernel(const uint32_t* 
     const uint4 v = kq[i];
     kw[4 * i] = v.x; kw[4 * i + 1] = v.y; kw[4 * i + 2] = v.z; kw[4 * i + 3] = v.w;
   }
-  fe x, y;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     x.v[i] = kw[i];
     y.v[i] = kw[9 + i];
   }
-  ge_p3 P, acc;
-  affine_to_p3(P, x, y);
-  ge_cached cP;
-  ge_p3_to_cached(cP, P);
-  ge_p3_0(acc);
-  ge_p1p1 t;
-  ge_p2 a2;
-#pragma unroll 1
-  for (int b = 7; b >= 0; --b) {
-    ge_p3_to_p2(a2, acc);
-    ge_p2_dbl(t, a2);
-    ge_p1p1_to_p3(acc, t);
-    if ((j >> b) & 1u) {
-      ge_add_cached(t, acc, cP);
-      ge_p1p1_to_p3(acc, t);
-    }
-  }
+}
+
+__global__ __launch_bounds__(kBlock) void key_table_wide_base_kernel(const uint32_t* __restrict__ counter,
+                                                                     uint32_t cnt, const uint4* __restrict__ keytab,
+                                                                     uint4* __restrict__ widetabs) {
+  const uint32_t nu = *counter;
+  if (!wide_keys(nu, cnt)) return;
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t u = g / (uint32_t)kWideBaseEntries, i = g % (uint32_t)kWideBaseEntries;
+  if (u >= nu) return;  // no wave-level collective in this kernel
+  fe x, y;
+  wide_key_point(x, y, keytab, u);
+  const int j = wide_base_index((int)i);
   ge_cached c;
-  ge_p3_to_cached(c, acc);
-  TableView::contiguous(widetabs + (size_t)u * (kWideKeyEntries * 9)).store((int)j, c);
+  small_multiple_cached(c, x, y, j);
+  TableView::contiguous(widetabs + (size_t)u * (kWideKeyEntries * 9)).store(j, c);
+}
+
+// Stage 2: one lane per (key u, entry j = 16b + a, b >= 1, a = 1..15):
+// entry 16b + entry a.
+__global__ __launch_bounds__(kBlock) void key_table_wide_pair_kernel(const uint32_t* __restrict__ counter,
+                                                                     uint32_t cnt, uint4* __restrict__ widetabs) {
+  const uint32_t nu = *counter;
+  if (!wide_keys(nu, cnt)) return;
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t u = g / (uint32_t)kWideKeyEntries, j = g % (uint32_t)kWideKeyEntries;
+  if (u >= nu || j < 16 || (j & 15u) == 0) return;  // no wave-level collective in this kernel
+  const TableView tv = TableView::contiguous(widetabs + (size_t)u * (kWideKeyEntries * 9));
+  ge_cached hi, lo, c;
+  tv.load((int)(j & ~15u), hi);
+  tv.load((int)(j & 15u), lo);
+  wide_pair_entry(c, hi, lo);
+  tv.store((int)j, c);
 }
 
 // Phase 1b with the keys already decoded: only R's square-root chain, so the
@@ -626,7 +634,7 @@ __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
   h.pad = uid;
   const uint32_t nu = *counter;
   if (nu <= kKeyTables) h.tops |= kHalfKeyed | c_neg;  // the main kernel reads the key's table
-  if (wide_keys(nu, kcnt)) h.tops |= kHalfKeyedWide;  // kcnt: the key domain's rows (key_table_wide_kernel's choice)
+  if (wide_keys(nu, kcnt)) h.tops |= kHalfKeyedWide;  // kcnt: the key domain's rows (key_table_wide_base_kernel's choice)
   if (live) {
     q[4] = make_uint4(w[16], w[17], w[18], w[19]);
     st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
@@ -1870,8 +1878,10 @@ static KeyDomain key_domain(uint4* ws, uint32_t grid) {
 
 // The dedup chain over rows [base, base+cnt) (cnt <= kPreChunk): hash slots,
 // owners, decoded keys, shared or wide key tables -- rep[i] for row base+i.
-static hipError_t launch_key_domain(const uint8_t* pk, uint32_t base, uint32_t cnt, const KeyDomain& kd,
-                                    hipStream_t stream) {
+// wcnt: the row count the wide-table choice sees (wide_keys): cnt, or 0 to
+// build the 9-entry tables only (VerifyExec::wide_min).
+static hipError_t launch_key_domain(const uint8_t* pk, uint32_t base, uint32_t cnt, uint32_t wcnt,
+                                    const KeyDomain& kd, hipStream_t stream) {
   const dim3 g1((cnt + kBlock - 1) / kBlock);
   uint32_t nslots = 64;
   while (nslots < 2 * cnt) nslots <<= 1;  // <= kDedupSlots
@@ -1882,12 +1892,23 @@ static hipError_t launch_key_domain(const uint8_t* pk, uint32_t base, uint32_t c
   hipLaunchKernelGGL(key_insert_kernel, g1, dim3(kBlock), 0, stream, pk, base, cnt, kd.kslots, nslots - 1, kd.rep,
                      kd.uid_of, kd.counter, kd.owners);
   hipLaunchKernelGGL(key_decode_kernel, g1, dim3(kBlock), 0, stream, pk, base, kd.counter, kd.owners, kd.keytab,
-                     kd.keytabs, cnt);
-  const uint32_t wmax = cnt / kWideKeyRepeat < kWideKeys ? cnt / kWideKeyRepeat : kWideKeys;  // keys that can be wide
-  if (wmax > 0)
-    hipLaunchKernelGGL(key_table_wide_kernel, dim3((wmax * (uint32_t)kWideKeyEntries + kBlock - 1) / kBlock),
-                       dim3(kBlock), 0, stream, kd.counter, cnt, kd.keytab, kd.widetabs);
+                     kd.keytabs, wcnt);
+  const uint32_t wmax = wcnt / kWideKeyRepeat < kWideKeys ? wcnt / kWideKeyRepeat : kWideKeys;  // keys that can be wide
+  if (wmax > 0) {
+    hipLaunchKernelGGL(key_table_wide_base_kernel, dim3((wmax * (uint32_t)kWideBaseEntries + kBlock - 1) / kBlock),
+                       dim3(kBlock), 0, stream, kd.counter, wcnt, kd.keytab, kd.widetabs);
+    hipLaunchKernelGGL(key_table_wide_pair_kernel, dim3((wmax * (uint32_t)kWideKeyEntries + kBlock - 1) / kBlock),
+                       dim3(kBlock), 0, stream, kd.counter, wcnt, kd.widetabs);
+  }
   return hipGetLastError();
+}
+
+static uint32_t wide_count(uint32_t cnt, uint32_t wide_min) { return cnt >= wide_min ? cnt : 0u; }
+
+hipError_t launch_key_domain_ws(const uint8_t* pk, uint32_t n, uint4* ws, uint32_t grid, uint32_t wide_min,
+                                hipStream_t stream) {
+  if (n == 0 || n > kPreChunk) return hipErrorInvalidValue;
+  return launch_key_domain(pk, 0, n, wide_count(n, wide_min), key_domain(ws, grid), stream);
 }
 
 // One chunk (<= kPreChunk signatures at [base, base+cnt)) on one stream and
@@ -1910,7 +1931,9 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
   const bool dedup = (policy & kModeDedupKeys) != 0;
   // a launch-wide key domain (KeyDomain: one key table for every chunk of
   // the launch, in x.key_ws) or this chunk's own, in its workspace
-  const KeyDomain kd = key_domain(x.key_ws ? x.key_ws : ws, grid);
+  // at the workspace's own offset: chunks of one call may differ in grid
+  // (verify_grid_for), the domain they share may not
+  const KeyDomain kd = key_domain(x.key_ws ? x.key_ws : ws, x.ws_grid ? x.ws_grid : grid);
   uint32_t* kslots = kd.kslots;
   uint32_t* rep = x.key_ws ? kd.rep + x.key_base + base : kd.rep;
   uint32_t* uid_of = kd.uid_of;
@@ -1919,7 +1942,8 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
   uint4* keytab = kd.keytab;
   uint4* keytabs = kd.keytabs;
   uint4* widetabs = kd.widetabs;
-  const uint32_t kcnt = x.key_ws ? x.key_n : cnt;  // rows of the key domain (the wide-table choice)
+  // rows of the key domain as the wide-table choice sees them
+  const uint32_t kcnt = wide_count(x.key_ws ? x.key_n : cnt, x.wide_min);
   {
     const dim3 g1((cnt + kBlock - 1) / kBlock);
     const uint32_t units = (cnt + 63) / 64;
@@ -1962,13 +1986,13 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
       // phase 1 done
     } else if (dedup) {
       if (!x.key_ws) {
-        hipError_t e = launch_key_domain(pk, base, cnt, kd, stream);
+        hipError_t e = launch_key_domain(pk, base, cnt, kcnt, kd, stream);
         if (e != hipSuccess) return e;
       } else if (x.key_build) {
         // the launch-wide domain, built once on this (the first) stream
         // after this chunk's scalar kernel, over every row of the launch
         hipError_t e = x.key_after ? hipStreamWaitEvent(stream, x.key_after, 0) : hipSuccess;
-        if (e == hipSuccess) e = launch_key_domain(pk, 0, x.key_n, kd, stream);
+        if (e == hipSuccess) e = launch_key_domain(pk, 0, x.key_n, kcnt, kd, stream);
         if (e == hipSuccess) e = hipEventRecord(x.key_ready, stream);
         if (e != hipSuccess) return e;
       } else {
@@ -2058,13 +2082,21 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
     xk.key_ws = x.ws[0];
     xk.key_base = 0;
     xk.key_n = n;
+    if (x.key_stream) {  // beside the chunks' scalar kernels, on its own stream
+      e = S > 1 ? hipStreamWaitEvent(x.key_stream, x.fork, 0) : hipSuccess;
+      if (e == hipSuccess)
+        e = launch_key_domain(pk, 0, n, wide_count(n, x.wide_min),
+                              key_domain(x.ws[0], x.ws_grid ? x.ws_grid : x.grid), x.key_stream);
+      if (e == hipSuccess) e = hipEventRecord(x.key_ready, x.key_stream);
+      if (e != hipSuccess) return e;
+    }
   }
   for (uint64_t c = 0; c < nchunks; ++c) {  // 64-bit: n may reach 2^32 - 64
     const uint32_t j = (uint32_t)(c % S);
     const uint32_t base = (uint32_t)(c * csize);
     const uint32_t cnt = n - base < csize ? n - base : csize;
     uint32_t* q = x.main_queue ? queue_counters(x.ws[j], x.grid) + c / S : nullptr;
-    if (shared_keys) xk.key_build = c == 0;
+    if (shared_keys) xk.key_build = c == 0 && !x.key_stream;
     e = verify_chunk(sig, msg_or_k, pk, base, cnt, bitmap, policy, pre_k, xk, x.streams[j], x.ws[j], q,
                      S > 1 ? nullptr : x.clock);
     if (e != hipSuccess) return e;
@@ -2120,7 +2152,7 @@ hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_
 
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
-                          hipStream_t stream, uint32_t kind_id) {
+                          hipStream_t stream, uint32_t kind_id, hipEvent_t parsed) {
   if (n == 0) return hipSuccess;
   const BlobKind kind = kind_id == 1u ? blob_kind_validation() : blob_kind_tx();
   uint4* layout = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qws) + blob_layout_offset(n));
@@ -2130,7 +2162,9 @@ hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint3
   const uint32_t pgrid = 2u * grid;
   hipLaunchKernelGGL(tx_blob_parse_kernel, dim3(blocks < pgrid ? blocks : pgrid), dim3(kBlock), 0, stream, blobs, off,
                      len, n, msg, sig, pk, txid, status, layout, side, kind);
-  hipError_t e = launch_order(len, n, kind.id_prefixed ? 4u : 0u, qws, stream);
+  hipError_t e = parsed ? hipEventRecord(parsed, stream) : hipSuccess;
+  if (e != hipSuccess) return e;
+  e = launch_order(len, n, kind.id_prefixed ? 4u : 0u, qws, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tx_blob_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, blobs, off, len,
                      n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4, layout, side, kind);

@@ -110,6 +110,12 @@ struct TableView {
     return TableView{head, tails, 8, tstride, id_head};
   }
   STL_HD const uint4* head(int e) const {
+#ifdef STL_EXP_TABLE_LINES
+    // timing-only (wrong results): a per-lane table of
+    // STL_EXP_TABLE_LINES head lines -- entries folded onto them -- bounds
+    // what any smaller table layout could gain from its footprint alone
+    if (id) return e == 0 ? id : main + ((e - 1) % STL_EXP_TABLE_LINES) * estride;
+#endif
     if (id) return e == 0 ? id : main + (e - 1) * estride;
     return main + e * estride;
   }
@@ -486,6 +492,73 @@ STL_HD void affine_to_p3(ge_p3& P, const fe& x, const fe& y) {
   P.Y = y;
   fe_1(P.Z);
   fe_mul(P.T, x, y);
+}
+
+// ---- wide per-key tables in two stages (round 6) ----
+// A key's wide table holds j*P, j = 0..136 (P = -A, kWideKeyEntries), in
+// cached form.  Stage 1 (one lane per key and i < kWideBaseEntries) builds the
+// 24 entries the others are sums of: a*P for a = 0..15 (entry a) and 16b*P
+// for b = 1..8 (entry 16b), by double-and-add; stage 2 (one lane per
+// remaining entry 16b + a, a = 1..15) adds entry a to entry 16b -- one
+// addition instead of the eight doublings and up to eight additions a lane
+// spent on its j before (key_table_wide_kernel: 96 us of config 1's 100k-row
+// call on the critical path).
+constexpr int kWideBaseEntries = 24;
+// the entry stage-1 lane i builds
+STL_HD int wide_base_index(int i) { return i < 16 ? i : 16 * (i - 15); }
+
+// 1/d (d = -121665/121666), canonical limbs
+STL_HD void fe_const_dinv(fe& h) {
+  const uint32_t c[9] = {0x0dc9f843u, 0x0f0793b6u, 0x1e550b89u, 0x1bad3084u, 0x1cf660b5u,
+                         0x108a66dcu, 0x190cac58u, 0x1a429ab9u, 0x0040907eu};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) h.v[i] = c[i];
+}
+
+// j*P for j < 256 by double-and-add over j's bits (P affine), cached form
+STL_HD void small_multiple_cached(ge_cached& out, const fe& x, const fe& y, int j) {
+  ge_p3 P, acc;
+  affine_to_p3(P, x, y);
+  ge_cached cP;
+  ge_p3_to_cached(cP, P);
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_p2 a2;
+#pragma unroll 1
+  for (int b = 7; b >= 0; --b) {
+    ge_p3_to_p2(a2, acc);
+    ge_p2_dbl(t, a2);
+    ge_p1p1_to_p3(acc, t);
+    if ((j >> b) & 1) {
+      ge_add_cached(t, acc, cP);
+      ge_p1p1_to_p3(acc, t);
+    }
+  }
+  ge_p3_to_cached(out, acc);
+}
+
+// A cached entry (Y+X, Y-X, Z, 2dT) back in extended coordinates, scaled by
+// 2: (2X : 2Y : 2Z : 2T) = (YpX - YmX, YpX + YmX, 2Z, T2d / d) -- a valid
+// representative of the same point (2X * 2Y == 2Z * 2T), one product.
+STL_HD void cached_to_p3x2(ge_p3& r, const ge_cached& c) {
+  fe_sub(r.X, c.YpX, c.YmX);
+  fe_add(r.Y, c.YpX, c.YmX);
+  fe_carry(r.Y);
+  fe_add(r.Z, c.Z, c.Z);
+  fe_carry(r.Z);
+  fe dinv;
+  fe_const_dinv(dinv);
+  fe_mul(r.T, c.T2d, dinv);
+}
+
+// entry 16b + a = entry 16b + entry a (stage 2)
+STL_HD void wide_pair_entry(ge_cached& out, const ge_cached& e16b, const ge_cached& ea) {
+  ge_p3 P, S;
+  cached_to_p3x2(P, e16b);
+  ge_p1p1 t;
+  ge_add_cached(t, P, ea);
+  ge_p1p1_to_p3(S, t);
+  ge_p3_to_cached(out, S);
 }
 
 // Positions the Straus loop must run for this wave: the largest need of its

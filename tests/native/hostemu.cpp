@@ -414,6 +414,59 @@ void hostemu_fe_mul_bytes(const uint8_t a[32], const uint8_t b[32], uint8_t out[
   std::memcpy(out, wo, 32);
 }
 
+// The wide per-key table j*(-A), j = 0..136, as the two-stage device build
+// makes it (key_table_wide_base_kernel: wide_base_index entries by
+// small_multiple_cached; key_table_wide_pair_kernel: wide_pair_entry), each
+// entry as affine (x, y) bytes; out_direct the same from double-and-add of
+// every j (the one-stage build it replaced).  Returns 0 if A does not decode.
+static void cached_affine_bytes(uint8_t out[64], const stl::ge_cached& c) {
+  stl::fe x2, y2, z2, zi, x, y;
+  stl::fe_sub(x2, c.YpX, c.YmX);
+  stl::fe_add(y2, c.YpX, c.YmX);
+  stl::fe_carry(y2);
+  stl::fe_add(z2, c.Z, c.Z);
+  stl::fe_carry(z2);
+  stl::fe_invert(zi, z2);
+  stl::fe_mul(x, x2, zi);
+  stl::fe_mul(y, y2, zi);
+  uint32_t wx[8], wy[8];
+  stl::fe_tobytes(wx, x);
+  stl::fe_tobytes(wy, y);
+  std::memcpy(out, wx, 32);
+  std::memcpy(out + 32, wy, 32);
+}
+
+int hostemu_wide_key_table(const uint8_t A_in[32], uint8_t* out_two_stage, uint8_t* out_direct) {
+  uint32_t A[8];
+  load8(A, A_in);
+  stl::ge_p3 negA;
+  if (!stl::ge_frombytes_negate_vartime(negA, A)) return 0;
+  std::vector<uint4> tab((size_t)stl::kWideKeyEntries * 9);
+  const stl::TableView tv = stl::TableView::contiguous(tab.data());
+  for (int i = 0; i < stl::kWideBaseEntries; ++i) {
+    stl::ge_cached c;
+    const int j = stl::wide_base_index(i);
+    stl::small_multiple_cached(c, negA.X, negA.Y, j);
+    tv.store(j, c);
+  }
+  for (int j = 17; j < stl::kWideKeyEntries; ++j) {
+    if ((j & 15) == 0) continue;
+    stl::ge_cached hi, lo, c;
+    tv.load(j & ~15, hi);
+    tv.load(j & 15, lo);
+    stl::wide_pair_entry(c, hi, lo);
+    tv.store(j, c);
+  }
+  for (int j = 0; j < stl::kWideKeyEntries; ++j) {
+    stl::ge_cached c, d;
+    tv.load(j, c);
+    cached_affine_bytes(out_two_stage + 64 * j, c);
+    stl::small_multiple_cached(d, negA.X, negA.Y, j);
+    cached_affine_bytes(out_direct + 64 * j, d);
+  }
+  return 1;
+}
+
 void hostemu_fe_invert_bytes(const uint8_t a[32], uint8_t out[32]) {
   uint32_t wa[8], wo[8];
   load8(wa, a);

@@ -286,6 +286,8 @@ def load_hostemu():
     lib.hostemu_signed_blob.argtypes = [ctypes.c_uint32, V, ctypes.c_uint32, V, V, V]
     lib.hostemu_blob_words.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, V]
     lib.hostemu_wide_row.argtypes = [ctypes.c_int, ctypes.c_uint32, V]
+    lib.hostemu_wide_key_table.restype = ctypes.c_int
+    lib.hostemu_wide_key_table.argtypes = [V, V, V]
     lib.hostemu_sign_adversarial.argtypes = [V, V, V, V, ctypes.c_size_t, V, V, V]
     lib.hostemu_window_blocks.restype = ctypes.c_uint32
     lib.hostemu_window_blocks.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]

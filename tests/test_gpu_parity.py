@@ -567,7 +567,8 @@ def test_shared_key_domain_same_bits(stl, golden, oracle, torch_cuda, policy):
     ONE key domain for all of them (STL_TUNE_SHARED_KEYS, default on): its
     first chunk builds the hash slots, decoded keys and wide / shared key
     tables over every row, the others wait for them.  Bits equal the
-    per-chunk domains' and the no-dedup path's, at sizes of 2 chunks (100k,
+    per-chunk domains', the 9-entry-only tables' (STL_TUNE_WIDE_MIN_ROWS) and
+    the no-dedup path's, at sizes of 2 chunks (100k,
     300k), 4 chunks (1M) and with wide (1,000 signers) and 9-entry (10,000
     signers on 100k rows: < 32 rows per key) tables, 5 % of rows mutated --
     and through the one-call checkSign from preimages."""
@@ -582,14 +583,19 @@ def test_shared_key_domain_same_bits(stl, golden, oracle, torch_cuda, policy):
         col = torch.from_numpy(rng.integers(0, 64, int(bad.sum()))).cuda()
         sigd[torch.from_numpy(np.nonzero(bad)[0]).cuda(), col] ^= 0x10
         got = {}
-        for shared in (1, 0):
+        # (shared domain, wide-table row minimum): 1 << 20 builds 9-entry tables only
+        for shared, wmin in ((1, 0), (0, 0), (1, 1 << 20)):
             old = stl.debug_tuning(stl.TUNE_SHARED_KEYS, shared)
+            oldw = stl.debug_tuning(stl.TUNE_WIDE_MIN_ROWS, wmin)
             try:
                 w = stl.verify_batch_device(sigd, msgs, pkd, policy=policy | stl.DEDUP_KEYS)
                 torch.cuda.synchronize()
-                got[shared] = stl.words_to_bool(w, n)
+                got[(shared, wmin)] = stl.words_to_bool(w, n)
             finally:
                 stl.debug_tuning(stl.TUNE_SHARED_KEYS, old)
+                stl.debug_tuning(stl.TUNE_WIDE_MIN_ROWS, oldw)
+        assert np.array_equal(got[(1, 0)], got[(1, 1 << 20)]), (n, signers)
+        got = {k[0]: v for k, v in got.items() if k[1] == 0}
         w = stl.verify_batch_device(sigd, msgs, pkd, policy=policy | stl.NO_AUTO_DEDUP)
         torch.cuda.synchronize()
         plain = stl.words_to_bool(w, n)
@@ -599,8 +605,14 @@ def test_shared_key_domain_same_bits(stl, golden, oracle, torch_cuda, policy):
         samp = rng.choice(n, 2000, replace=False)
         s_np, m_np, p_np = sigd.cpu().numpy(), msgs.cpu().numpy(), pkd.cpu().numpy()
         assert np.array_equal(got[1][samp], oracle.verify_batch(s_np[samp], m_np[samp], p_np[samp], policy=policy))
-    # one-call checkSign over preimages, 2 chunks, forced dedup, shared vs not
-    n = 150_000
+    # one-call checkSign over preimages, 2 chunks, forced dedup, shared vs not;
+    # 99,968 rows: chunks of 50,048 and 49,920 rows whose verify grids differ
+    # (196 vs 195 workgroups' worth) while they share one key domain
+    for n in (150_000, 99_968):
+        _one_call_shared_keys(stl, torch, rng, n, policy)
+
+
+def _one_call_shared_keys(stl, torch, rng, n, policy):
     lens = rng.integers(113, 1500, n).astype(np.int32)
     offs = np.zeros(n, np.int64)
     offs[1:] = np.cumsum(lens[:-1])

@@ -96,3 +96,39 @@ def test_rows_match_python(emu, j):
         assert limbs_to_int(r[9:18]) == (y - x) % P
         assert limbs_to_int(r[18:27]) == 2 * D * x * y % P
         assert max(r[:27]) < 2**29 and r[27] == 0
+
+
+def _encode(pt):
+    x, y = pt
+    return (y | ((x & 1) << 255)).to_bytes(32, "little")
+
+
+@pytest.mark.parametrize("m", [5, 2**200 + 12345, L - 1])
+def test_wide_key_table_two_stages(emu, m):
+    """Round 6: the wide per-key tables j*(-A), j = 0..136, are built in two
+    stages (24 entries by double-and-add, the other 113 as one addition of two
+    of them: key_table_wide_base_kernel / key_table_wide_pair_kernel).  On the
+    host build of the same functions every entry equals the one-stage
+    double-and-add of j and -j*m*B computed in Python, for keys A = m*B."""
+    B = base_point()
+    A = ed_mul(m, B)
+    two = (ctypes.c_uint8 * (137 * 64))()
+    one = (ctypes.c_uint8 * (137 * 64))()
+    assert emu.hostemu_wide_key_table(_encode(A), two, one) == 1
+    assert bytes(two) == bytes(one)
+    for j in (0, 1, 15, 16, 17, 31, 33, 100, 128, 129, 136):
+        x, y = ed_mul(j * m % L, B) if j else (0, 1)
+        want = ((P - x) % P).to_bytes(32, "little") + y.to_bytes(32, "little")
+        assert bytes(two[64 * j:64 * j + 64]) == want, j
+
+
+def test_wide_key_table_small_order_key(emu):
+    """A key of order 8 (torsion, golden class B6-B8 material): the two-stage
+    table equals the double-and-add one for every j (the additions meet equal
+    and opposite points and the identity -- the complete formula's cases)."""
+    # an order-8 point: x^2 = ... pick the encoding from the small-order list
+    enc = bytes.fromhex("c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a")
+    two = (ctypes.c_uint8 * (137 * 64))()
+    one = (ctypes.c_uint8 * (137 * 64))()
+    assert emu.hostemu_wide_key_table(enc, two, one) == 1
+    assert bytes(two) == bytes(one)

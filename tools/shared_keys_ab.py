@@ -1,5 +1,6 @@
 """A/B of the launch-wide key domain (STL_TUNE_SHARED_KEYS 1) against one
-key domain per chunk (0), interleaved in one process: configs[0]'s 100k
+key domain per chunk (0), and of the wide key tables' row minimum
+(STL_TUNE_WIDE_MIN_ROWS), interleaved in one process: configs[0]'s 100k
 Payment blobs in one stl_signed_blob_verify_batch_device call (automatic
 dedup: 1,000 accounts), config 5's 2^20-preimage ledger in one
 stl_tx_verify_batch_device call, and a 1M / 300k verify with forced dedup.
@@ -60,26 +61,36 @@ def main():
         "config5_verify_100k_dedup": lambda: V.verify_batch_device(sig5[:100000], m5[:100000], pk5[:100000],
                                                                    out_words=w5, policy=V.DEDUP_KEYS, stream=s),
     }
+    # settings: (shared key domain, wide-table minimum rows)
+    settings = {"shared": (1, 0), "per_chunk": (0, 0), "shared_no_wide_below_400k": (1, 400000)}
+    if os.environ.get("AB_SETTINGS"):
+        settings = {k: v for k, v in settings.items() if k in os.environ["AB_SETTINGS"].split(",")}
+
+    def apply(v):
+        V.debug_tuning(V.TUNE_SHARED_KEYS, v[0])
+        V.debug_tuning(V.TUNE_WIDE_MIN_ROWS, v[1])
     out = {}
+    names = list(settings)
     for name, fn in cases.items():
-        ts = {0: [], 1: []}
-        for shared in (1, 0):
-            V.debug_tuning(V.TUNE_SHARED_KEYS, shared)
+        ts = {k: [] for k in names}
+        for k in names:
+            apply(settings[k])
             fn()
             fn()
         torch.cuda.synchronize()
         for r in range(reps):
-            for shared in ((1, 0) if r % 2 == 0 else (0, 1)):
-                V.debug_tuning(V.TUNE_SHARED_KEYS, shared)
+            order = names[r % len(names):] + names[:r % len(names)]
+            for k in (order if r % 2 == 0 else order[::-1]):
+                apply(settings[k])
                 fn()  # the automatic dedup follows the previous call's sample
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 fn()
                 torch.cuda.synchronize()
-                ts[shared].append(time.perf_counter() - t0)
-        out[name] = {f"shared{k}_ms": float(np.median(v)) * 1e3 for k, v in ts.items()}
-        print(name, out[name], file=sys.stderr, flush=True)
-    V.debug_tuning(V.TUNE_SHARED_KEYS, 1)
+                ts[k].append(time.perf_counter() - t0)
+        out[name] = {f"{k}_ms": float(np.median(v)) * 1e3 for k, v in ts.items()}
+        print(name, {k: round(v, 3) for k, v in out[name].items()}, file=sys.stderr, flush=True)
+    apply((1, 0))
     print(json.dumps(out))
 
 
