@@ -461,6 +461,9 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
 #define STL_TUNE_WIDE_MIN_ROWS 10     /* 0..2^20 (default 0): a key table of fewer rows (STL_DEDUP_KEYS or the
                                         automatic choice) builds the 9-entry per-key tables only, never
                                         the wide 137-entry ones (whose build a short call waits for) */
+#define STL_TUNE_R_AHEAD 11          /* 0 / 1 (default 1): a one-call checkSign with a shared key table
+                                        decodes every row's R on its own stream beside the key table's
+                                        build, and the chunks' phase 1 then only combines the two */
 #define STL_TUNE_RCCL_TIMEOUT_MS 7 /* 1..3,600,000 (default 120,000; env STL_RCCL_TIMEOUT_S): deadline of
                                       stl_comm_init_rank and stl_comm_sync */
 int stl_debug_tuning(int key, int value);

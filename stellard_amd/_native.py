@@ -47,6 +47,7 @@ STL_TUNE_RCCL_TIMEOUT_MS = 7
 STL_TUNE_LONG_HASH = 8
 STL_TUNE_SHARED_KEYS = 9
 STL_TUNE_WIDE_MIN_ROWS = 10
+STL_TUNE_R_AHEAD = 11
 
 # per-transaction status of the serialized-transaction entry points
 STL_TX_OK = 0

@@ -280,6 +280,7 @@ std::atomic<int> g_tune_quad{3};      // smallest chunks' main kernel on lane gr
 std::atomic<int> g_tune_long_hash{8}; // small batches: rows of more than this many blocks hashed one per wave (0 off)
 std::atomic<int> g_tune_shared_keys{1}; // key dedup over several chunks: one key domain per call (0: one per chunk)
 std::atomic<int> g_tune_wide_min{0};    // key domains of fewer rows build no wide key tables (the 9-entry ones)
+std::atomic<int> g_tune_r_ahead{1};     // one-call checkSign with a shared key domain: R decoded ahead on its own stream
 
 // Rows per step of verify time: the device-resident verify runs a chunk's
 // 64-signature units on its resident waves, two per SIMD, so its time rises in
@@ -353,6 +354,10 @@ struct StreamCtx {
   // one-call blob path's two parse kernels are done (the keys are out)
   hipEvent_t keys = nullptr;
   hipEvent_t parsed[2] = {};
+  // R decoded ahead for the one-call checkSign's shared key domain
+  // (stl::VerifyExec::rdec: 80 B per row) and its ready event
+  DevBuf rdec;
+  hipEvent_t rready = nullptr;
   // device-resident automatic dedup: host-mapped word the key sample kernel
   // writes after each call on this stream (1 = its keys repeated); the next
   // call reads it without waiting (feedback, so a stale value only picks the
@@ -380,11 +385,15 @@ struct StreamCtx {
       if (e) (void)hipEventDestroy(e);
       e = nullptr;
     }
+    rdec.release();
+    if (rready) (void)hipEventDestroy(rready);
+    rready = nullptr;
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
   }
   bool holds_memory() const {
-    return auto_flag || scratch.p || ws.p || queue.p || fork || keys || parsed[0] || parsed[1] || done;
+    return auto_flag || scratch.p || ws.p || queue.p || fork || keys || parsed[0] || parsed[1] || rdec.p || rready ||
+           done;
   }
   // moves every buffer and event of `o` into this (empty) context
   void adopt(StreamCtx& o) {
@@ -395,6 +404,8 @@ struct StreamCtx {
     std::swap(keys, o.keys);
     std::swap(parsed[0], o.parsed[0]);
     std::swap(parsed[1], o.parsed[1]);
+    std::swap(rdec, o.rdec);
+    std::swap(rready, o.rready);
     for (uint32_t j = 0; j < stl::kMaxVerifyStreams; ++j) std::swap(join[j], o.join[j]);
     std::swap(auto_flag, o.auto_flag);
     std::swap(auto_flag_dev, o.auto_flag_dev);
@@ -1525,6 +1536,9 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_SHARED_KEYS:
       if (value != 0 && value != 1) return STL_EINVAL;
       return g_tune_shared_keys.exchange(value);
+    case STL_TUNE_R_AHEAD:
+      if (value != 0 && value != 1) return STL_EINVAL;
+      return g_tune_r_ahead.exchange(value);
     case STL_TUNE_WIDE_MIN_ROWS:
       if (value < 0 || value > (int)stl::kPreChunk) return STL_EINVAL;
       return g_tune_wide_min.exchange(value);
@@ -1877,6 +1891,15 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   if (cs && blob)
     for (hipEvent_t& e : c.parsed)
       if (!e) STL_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // ... and R's decoding of every row on a fourth stream (the copy stream,
+  // idle in a device-resident call), beside the key domain: the chunks then
+  // finish their phase 1 without a square-root chain (VerifyExec::rdec)
+  hipStream_t cr = cs && g_tune_r_ahead.load() && d.copy != cs && d.copy != ks[0] && d.copy != ks[1] ? d.copy
+                                                                                                      : nullptr;
+  if (cr) {
+    STL_RC(c.rdec.ensure(n * 80));
+    if (!c.rready) STL_TRY(hipEventCreateWithFlags(&c.rready, hipEventDisableTiming));
+  }
   if (S > 1 || ahead) {
     if (!c.fork) STL_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
     if (!c.join[1]) STL_TRY(hipEventCreateWithFlags(&c.join[1], hipEventDisableTiming));
@@ -1887,6 +1910,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
   auto fail = [&](int rc) {
     if (S > 1 || ahead) (void)hipStreamSynchronize(ks[1]);
     if (cs) (void)hipStreamSynchronize(cs);
+    if (cr) (void)hipStreamSynchronize(cr);
     return rc;
   };
   if (ahead) {
@@ -1936,6 +1960,19 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     if (e == hipSuccess) e = hipEventRecord(c.keys, cs);
     if (e != hipSuccess) return fail(STL_EHIP);
   }
+  if (cr) {  // R's decoding of every row, as soon as the signatures are known
+    hipError_t e = hipSuccess;
+    if (blob) {
+      e = hipStreamWaitEvent(cr, c.parsed[0], 0);
+      if (e == hipSuccess) e = hipStreamWaitEvent(cr, c.parsed[1], 0);
+    } else {
+      e = hipStreamWaitEvent(cr, c.fork, 0);
+    }
+    if (e == hipSuccess && fault_now()) e = hipErrorUnknown;
+    if (e == hipSuccess) e = stl::launch_point_r(sig, pk, (uint32_t)n, mode, static_cast<uint4*>(c.rdec.p), cr);
+    if (e == hipSuccess) e = hipEventRecord(c.rready, cr);
+    if (e != hipSuccess) return fail(STL_EHIP);
+  }
   size_t k = 0;
   for (size_t b0 = 0; b0 < n; b0 += sub, ++k) {
     const uint32_t j = (uint32_t)(k % S);
@@ -1956,6 +1993,10 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
       x.key_build = k == 0 && !cs;
       x.key_ready = c.keys;
       x.key_after = blob && !cs ? c.join[2] : nullptr;
+      if (cr) {
+        x.rdec = static_cast<const uint4*>(c.rdec.p);
+        x.r_ready = c.rready;
+      }
     }
     x.wide_min = (uint32_t)g_tune_wide_min.load();
     if (fault_now() || stl::launch_verify(sig + 64 * b0, msg + 32 * b0, pk + 32 * b0, cnt, words + b0 / 64, mode,

@@ -126,7 +126,16 @@ struct VerifyExec {
   // the 9-entry ones instead -- so a short call does not wait for the wide
   // build (STL_TUNE_WIDE_MIN_ROWS)
   uint32_t wide_min = 0;
+  // With key_ws: R decoded ahead for every row of the key domain
+  // (launch_point_r, 5 quads per row, recording r_ready): the chunks run the
+  // short verify_finish_keyed_kernel instead of the keyed point kernel
+  const uint4* rdec = nullptr;
+  hipEvent_t r_ready = nullptr;
 };
+// The pre-checks and R's decoding of rows [0, n) into rdec (5 quads per row),
+// for VerifyExec::rdec.
+hipError_t launch_point_r(const uint8_t* sig, const uint8_t* pk, uint32_t n, uint32_t policy, uint4* rdec,
+                          hipStream_t stream);
 // The dedup chain over rows [0, n) of pk into the key domain of workspace ws
 // (grid: its resident workgroups) on `stream` -- what a chunk with
 // kModeDedupKeys builds for itself, for a caller that runs it beside other

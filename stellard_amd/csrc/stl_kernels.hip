@@ -593,6 +593,98 @@ __global__ __launch_bounds__(kBlock) void key_table_wide_pair_kernel(const uint3
   tv.store((int)j, c);
 }
 
+// The keyed point half split in two (round 6), so that R's square-root chain
+// runs while the key domain is still being built instead of after it:
+//   verify_point_r_kernel      rows [0, n) of a call, one lane each: the
+//                              pre-checks, stellard's S < L, R canonical and
+//                              R's decoding -Q, into rdec[i] (5 quads: -Q x, y,
+//                              word 18 = all of them passed);
+//   verify_finish_keyed_kernel a chunk's rows once rdec and the key domain are
+//                              ready: -A from the key table, then exactly the
+//                              state verify_point_kernel_keyed writes.
+// verify_phase1_points_keyed is the same computation in one lane.
+__global__ __launch_bounds__(kBlock, 4) void verify_point_r_kernel(const uint8_t* __restrict__ sig,
+                                                                   const uint8_t* __restrict__ pk, uint32_t n,
+                                                                   uint32_t policy, uint4* __restrict__ rdec) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= n) return;  // no wave-level collective in this kernel
+  uint32_t R[8], S[8], A[8];
+  ld8(R, sig + 64 * (size_t)t);
+  ld8(S, sig + 64 * (size_t)t + 32);
+  ld8(A, pk + 32 * (size_t)t);
+  const uint32_t pol = core_policy(policy);
+  bool ok = verify_prechecks(R, S, A, pol);
+  ok = ok && composite_s_ok(S, pol) && r_is_canonical(R);
+  ge_p3 negQ;
+  const bool okR = ge_frombytes_negate_vartime(negQ, R);
+  uint32_t w[20];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    w[i] = negQ.X.v[i];
+    w[9 + i] = negQ.Y.v[i];
+  }
+  w[18] = ok && okR ? 1u : 0u;
+  w[19] = 0;
+  uint4* q = rdec + (size_t)t * 5;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+__global__ __launch_bounds__(kBlock, 4) void verify_finish_keyed_kernel(
+    uint32_t cnt, uint32_t policy, uint4* __restrict__ pre, uint64_t* __restrict__ fb_words,
+    const uint32_t* __restrict__ rep, const uint32_t* __restrict__ uid_of, const uint4* __restrict__ keytab,
+    const uint32_t* __restrict__ counter, uint32_t kcnt, const uint4* __restrict__ rdec) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = t < cnt;
+  const uint32_t tt = live ? t : cnt - 1;
+  const uint32_t uid = uid_of[rep[tt]];
+  uint32_t kw[20], rw[20];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint4 v = keytab[(size_t)uid * 5 + i];
+    kw[4 * i] = v.x; kw[4 * i + 1] = v.y; kw[4 * i + 2] = v.z; kw[4 * i + 3] = v.w;
+    const uint4 r = rdec[(size_t)tt * 5 + i];
+    rw[4 * i] = r.x; rw[4 * i + 1] = r.y; rw[4 * i + 2] = r.z; rw[4 * i + 3] = r.w;
+  }
+  fe nAx, nAy, nQx, nQy;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    nAx.v[i] = kw[i];
+    nAy.v[i] = kw[9 + i];
+    nQx.v[i] = rw[i];
+    nQy.v[i] = rw[9 + i];
+  }
+  uint4* q = pre + (size_t)tt * 14;
+  HalfState h;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&h);
+  const uint4 q2 = q[kHalfTopsWord / 4], q4 = q[4];
+  w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+  w[16] = q4.x; w[17] = q4.y; w[18] = q4.z;
+  const uint32_t c_neg = h.tops & kHalfCNeg;
+  finish_phase1_points(h, nAx, nAy, nQx, nQy, rw[18] != 0 && kw[18] != 0);
+  if ((policy & kModeFullLength) && (h.tops & kHalfOk)) h.tops |= kHalfFallback;
+  h.pad = uid;
+  const uint32_t nu = *counter;
+  if (nu <= kKeyTables) h.tops |= kHalfKeyed | c_neg;  // the main kernel reads the key's table
+  if (wide_keys(nu, kcnt)) h.tops |= kHalfKeyedWide;
+  if (live) {
+    q[4] = make_uint4(w[16], w[17], w[18], w[19]);
+    st_state(q + kHalfTopsWord / 4, make_uint4(w[8], w[9], w[10], w[11]));
+#pragma unroll
+    for (int i = kHalfScalarQuads; i < 14; ++i) st_state(q + i, make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+  }
+  const uint64_t fb = __ballot(live && (h.tops & kHalfFallback) != 0);
+  if ((threadIdx.x & 63u) == 0 && t < cnt) fb_words[t >> 6] = fb;
+}
+
+hipError_t launch_point_r(const uint8_t* sig, const uint8_t* pk, uint32_t n, uint32_t policy, uint4* rdec,
+                          hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(verify_point_r_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, sig, pk, n,
+                     policy, rdec);
+  return hipGetLastError();
+}
+
 // Phase 1b with the keys already decoded: only R's square-root chain, so the
 // kernel runs at more waves per SIMD than the paired one.
 __global__ __launch_bounds__(kBlock, 4) void verify_point_kernel_keyed(
@@ -1999,8 +2091,15 @@ static hipError_t verify_chunk(const uint8_t* sig, const uint8_t* msg_or_k, cons
         hipError_t e = hipStreamWaitEvent(stream, x.key_ready, 0);
         if (e != hipSuccess) return e;
       }
-      hipLaunchKernelGGL(verify_point_kernel_keyed, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb,
-                         rep, uid_of, keytab, counter, kcnt);
+      if (x.key_ws && x.rdec) {  // R decoded ahead (VerifyExec::rdec)
+        hipError_t e = hipStreamWaitEvent(stream, x.r_ready, 0);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(verify_finish_keyed_kernel, g1, dim3(kBlock), 0, stream, cnt, policy, pre, fb, rep, uid_of,
+                           keytab, counter, kcnt, x.rdec + (size_t)(x.key_base + base) * 5);
+      } else {
+        hipLaunchKernelGGL(verify_point_kernel_keyed, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre,
+                           fb, rep, uid_of, keytab, counter, kcnt);
+      }
     } else {
       hipLaunchKernelGGL(verify_point_kernel, g1, dim3(kBlock), 0, stream, sig, pk, base, cnt, policy, pre, fb);
     }

@@ -605,6 +605,7 @@ TUNE_RCCL_TIMEOUT_MS = N.STL_TUNE_RCCL_TIMEOUT_MS
 TUNE_LONG_HASH = N.STL_TUNE_LONG_HASH
 TUNE_SHARED_KEYS = N.STL_TUNE_SHARED_KEYS
 TUNE_WIDE_MIN_ROWS = N.STL_TUNE_WIDE_MIN_ROWS
+TUNE_R_AHEAD = N.STL_TUNE_R_AHEAD
 
 
 def debug_tuning(key, value):
@@ -679,7 +680,8 @@ def execution_settings():
     return {name: lib.stl_debug_tuning(key, -1) for name, key in (
         ("fused_prep", TUNE_FUSED_PREP), ("main_queue", TUNE_MAIN_QUEUE), ("streams", TUNE_STREAMS),
         ("chunk_log2", TUNE_CHUNK_LOG2), ("quad", TUNE_QUAD), ("long_hash", TUNE_LONG_HASH),
-        ("shared_keys", TUNE_SHARED_KEYS), ("wide_min_rows", TUNE_WIDE_MIN_ROWS))}
+        ("shared_keys", TUNE_SHARED_KEYS), ("wide_min_rows", TUNE_WIDE_MIN_ROWS),
+        ("r_ahead", TUNE_R_AHEAD))}
 
 
 def sign_batch_device(seed, msg, stream=None):

@@ -626,15 +626,18 @@ def _one_call_shared_keys(stl, torch, rng, n, policy):
     bad = rng.random(n) < 0.03
     sigd[torch.from_numpy(np.nonzero(bad)[0]).cuda(), 50] ^= 0x04
     outs = []
-    for shared in (1, 0):
+    # (shared domain, R decoded ahead on its own stream)
+    for shared, ahead in ((1, 1), (1, 0), (0, 0)):
         old = stl.debug_tuning(stl.TUNE_SHARED_KEYS, shared)
+        olda = stl.debug_tuning(stl.TUNE_R_AHEAD, ahead)
         try:
             w = stl.tx_verify_batch_device(d_pre, d_off, d_len, sigd, pkd, policy=policy | stl.DEDUP_KEYS)
             torch.cuda.synchronize()
             outs.append(stl.words_to_bool(w, n))
         finally:
             stl.debug_tuning(stl.TUNE_SHARED_KEYS, old)
-    assert np.array_equal(outs[0], outs[1])
+            stl.debug_tuning(stl.TUNE_R_AHEAD, olda)
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
     assert np.array_equal(outs[0], ~bad)
 
 

@@ -61,14 +61,15 @@ def main():
         "config5_verify_100k_dedup": lambda: V.verify_batch_device(sig5[:100000], m5[:100000], pk5[:100000],
                                                                    out_words=w5, policy=V.DEDUP_KEYS, stream=s),
     }
-    # settings: (shared key domain, wide-table minimum rows)
-    settings = {"shared": (1, 0), "per_chunk": (0, 0), "shared_no_wide_below_400k": (1, 400000)}
+    # settings: (shared key domain, wide-table minimum rows, R decoded ahead)
+    settings = {"shared": (1, 0, 1), "shared_r_inline": (1, 0, 0), "per_chunk": (0, 0, 0)}
     if os.environ.get("AB_SETTINGS"):
         settings = {k: v for k, v in settings.items() if k in os.environ["AB_SETTINGS"].split(",")}
 
     def apply(v):
         V.debug_tuning(V.TUNE_SHARED_KEYS, v[0])
         V.debug_tuning(V.TUNE_WIDE_MIN_ROWS, v[1])
+        V.debug_tuning(V.TUNE_R_AHEAD, v[2])
     out = {}
     names = list(settings)
     for name, fn in cases.items():
@@ -90,7 +91,7 @@ def main():
                 ts[k].append(time.perf_counter() - t0)
         out[name] = {f"{k}_ms": float(np.median(v)) * 1e3 for k, v in ts.items()}
         print(name, {k: round(v, 3) for k, v in out[name].items()}, file=sys.stderr, flush=True)
-    apply((1, 0))
+    apply((1, 0, 1))
     print(json.dumps(out))
 
 
