@@ -1923,9 +1923,27 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     if (rc) return fail(rc);
   }
   // rows [b0, b0 + cnt) hashed (or passed) on stream js with queue qw
-  auto hash = [&](size_t b0, size_t cnt, hipStream_t js, uint32_t* qw) -> int {
+  // blob rows' pass in two halves when the key work runs beside it: both
+  // streams' parse kernels first (the keys and signatures are out), then the
+  // key domain and R's decoding are enqueued, then the hashing -- so the
+  // host's enqueue order follows the device's critical path
+  const bool split_pass = blob && cs && S > 1;
+  auto parse = [&](size_t b0, size_t cnt, hipStream_t js, uint32_t* qw) -> int {
     if (fault_now()) return STL_EHIP;
+    const hipError_t e = stl::launch_tx_blob_parse(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0,
+                                                   sig + 64 * b0, pk + 32 * b0, id ? id + 32 * b0 : nullptr, st + b0,
+                                                   qw, hash_grid(d), js, kind, c.parsed[js == ks[0] ? 0 : 1]);
+    return e == hipSuccess ? STL_OK : STL_EHIP;
+  };
+  // rows [b0, b0 + cnt) hashed (or passed) on stream js with queue qw
+  auto hash = [&](size_t b0, size_t cnt, hipStream_t js, uint32_t* qw) -> int {
     hipError_t e;
+    if (split_pass) {
+      e = stl::launch_tx_blob_hash(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, sig + 64 * b0,
+                                   pk + 32 * b0, id ? id + 32 * b0 : nullptr, st + b0, qw, hash_grid(d), js, kind);
+      return e == hipSuccess ? STL_OK : STL_EHIP;
+    }
+    if (fault_now()) return STL_EHIP;
     if (blob)
       e = stl::launch_tx_blob(bytes, off + b0, len + b0, (uint32_t)cnt, msg + 32 * b0, sig + 64 * b0, pk + 32 * b0,
                               id ? id + 32 * b0 : nullptr, st + b0, qw, hash_grid(d), js, kind,
@@ -1935,15 +1953,23 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
                               hash_long_min(d, n));
     return e == hipSuccess ? STL_OK : STL_EHIP;
   };
-  if (S == 1) {
-    int rc = hash(0, n, s, q[0]);
-    if (!rc && ahead && hipStreamWaitEvent(s, c.join[2], 0) != hipSuccess) rc = STL_EHIP;
-    if (rc) return fail(rc);
-  } else {
+  auto hash_all = [&]() -> int {
+    if (S == 1) {
+      int rc = hash(0, n, s, q[0]);
+      if (!rc && ahead && hipStreamWaitEvent(s, c.join[2], 0) != hipSuccess) rc = STL_EHIP;
+      return rc;
+    }
     int rc = hash(0, sub, ks[0], q[0]);
     if (!rc) rc = hash(sub, n - sub, ks[1], q[1]);
     if (!rc && hipEventRecord(c.join[2], ks[1]) != hipSuccess) rc = STL_EHIP;
+    return rc;
+  };
+  if (split_pass) {
+    int rc = parse(0, sub, ks[0], q[0]);
+    if (!rc) rc = parse(sub, n - sub, ks[1], q[1]);
     if (rc) return fail(rc);
+  } else if (int rc = hash_all()) {
+    return fail(rc);
   }
   if (cs) {  // the call's key domain on its own stream, in the caller's workspace
     hipError_t e = hipSuccess;
@@ -1973,6 +1999,8 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     if (e == hipSuccess) e = hipEventRecord(c.rready, cr);
     if (e != hipSuccess) return fail(STL_EHIP);
   }
+  if (split_pass)
+    if (int rc = hash_all()) return fail(rc);
   size_t k = 0;
   for (size_t b0 = 0; b0 < n; b0 += sub, ++k) {
     const uint32_t j = (uint32_t)(k % S);

@@ -177,6 +177,13 @@ hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_
 hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
                           uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
                           hipStream_t stream, uint32_t kind = 0u /* STL_BLOB_* */, hipEvent_t parsed = nullptr);
+// its two halves: the parse kernel (+ `parsed`), then the ordering and hashing
+hipError_t launch_tx_blob_parse(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n,
+                                uint8_t* msg, uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status,
+                                uint32_t* qws, uint32_t grid, hipStream_t stream, uint32_t kind, hipEvent_t parsed);
+hipError_t launch_tx_blob_hash(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n,
+                               uint8_t* msg, uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status,
+                               uint32_t* qws, uint32_t grid, hipStream_t stream, uint32_t kind);
 // Wide base tables (stl_verify_core.h): 2 * 32769 rows of 28 words.
 constexpr size_t kWideTableBytes = 2ull * 32769 * 28 * 4;
 // Key-repeat sample of [0, n): *flag = 1 when a quarter of up to 2,048 sampled

@@ -461,11 +461,24 @@ hipError_t launch_clock_stamp(unsigned long long* out, uint32_t nwg, hipStream_t
   return hipGetLastError();
 }
 
+// The key-dedup chain (insert, decode, wide tables) is a few latency-bound
+// waves (one lane per distinct key) that gate every chunk of a call, while
+// the chunks' own phase-1 kernels fill the same SIMDs: its waves raise their
+// issue priority (s_setprio, wave-level arbitration only) so their dependent
+// chains do not queue behind the co-resident waves.
+#ifndef STL_CHAIN_PRIO
+#define STL_CHAIN_PRIO 3
+#endif
+__device__ __forceinline__ void chain_priority() {
+  if (STL_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(STL_CHAIN_PRIO);
+}
+
 __global__ __launch_bounds__(kBlock) void key_insert_kernel(const uint8_t* __restrict__ pk, uint32_t base,
                                                             uint32_t cnt, uint32_t* __restrict__ slots, uint32_t mask,
                                                             uint32_t* __restrict__ rep, uint32_t* __restrict__ uid_of,
                                                             uint32_t* __restrict__ counter,
                                                             uint32_t* __restrict__ owners) {
+  chain_priority();
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const bool live = t < cnt;
@@ -516,6 +529,7 @@ __global__ __launch_bounds__(kBlock, 4) void key_decode_kernel(const uint8_t* __
                                                                const uint32_t* __restrict__ owners,
                                                                uint4* __restrict__ keytab,
                                                                uint4* __restrict__ keytabs, uint32_t cnt) {
+  chain_priority();
   const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t nu = *counter;
   if (u >= nu) return;  // no wave-level collective in this kernel
@@ -563,6 +577,7 @@ __device__ __forceinline__ void wide_key_point(fe& x, fe& y, const uint4* __rest
 __global__ __launch_bounds__(kBlock) void key_table_wide_base_kernel(const uint32_t* __restrict__ counter,
                                                                      uint32_t cnt, const uint4* __restrict__ keytab,
                                                                      uint4* __restrict__ widetabs) {
+  chain_priority();
   const uint32_t nu = *counter;
   if (!wide_keys(nu, cnt)) return;
   const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
@@ -580,6 +595,7 @@ __global__ __launch_bounds__(kBlock) void key_table_wide_base_kernel(const uint3
 // entry 16b + entry a.
 __global__ __launch_bounds__(kBlock) void key_table_wide_pair_kernel(const uint32_t* __restrict__ counter,
                                                                      uint32_t cnt, uint4* __restrict__ widetabs) {
+  chain_priority();
   const uint32_t nu = *counter;
   if (!wide_keys(nu, cnt)) return;
   const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
@@ -2249,9 +2265,15 @@ hipError_t launch_tx_hash(const uint8_t* pre, const uint64_t* off, const uint32_
   return hipGetLastError();
 }
 
-hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
-                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
-                          hipStream_t stream, uint32_t kind_id, hipEvent_t parsed) {
+// The blob pass in two halves (the one-call checkSign enqueues both rows'
+// parse kernels, then the key work that needs only their keys, then the
+// hashing): launch_tx_blob_parse writes status, layout, signature and key of
+// every row (and records `parsed`), launch_tx_blob_hash orders the rows and
+// hashes them.
+hipError_t launch_tx_blob_parse(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n,
+                                uint8_t* msg, uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status,
+                                uint32_t* qws, uint32_t grid, hipStream_t stream, uint32_t kind_id,
+                                hipEvent_t parsed) {
   if (n == 0) return hipSuccess;
   const BlobKind kind = kind_id == 1u ? blob_kind_validation() : blob_kind_tx();
   uint4* layout = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qws) + blob_layout_offset(n));
@@ -2261,13 +2283,33 @@ hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint3
   const uint32_t pgrid = 2u * grid;
   hipLaunchKernelGGL(tx_blob_parse_kernel, dim3(blocks < pgrid ? blocks : pgrid), dim3(kBlock), 0, stream, blobs, off,
                      len, n, msg, sig, pk, txid, status, layout, side, kind);
-  hipError_t e = parsed ? hipEventRecord(parsed, stream) : hipSuccess;
-  if (e != hipSuccess) return e;
-  e = launch_order(len, n, kind.id_prefixed ? 4u : 0u, qws, stream);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && parsed) e = hipEventRecord(parsed, stream);
+  return e;
+}
+
+hipError_t launch_tx_blob_hash(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n,
+                               uint8_t* msg, uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status,
+                               uint32_t* qws, uint32_t grid, hipStream_t stream, uint32_t kind_id) {
+  if (n == 0) return hipSuccess;
+  const BlobKind kind = kind_id == 1u ? blob_kind_validation() : blob_kind_tx();
+  uint4* layout = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qws) + blob_layout_offset(n));
+  uint4* side = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qws) + blob_side_offset(n));
+  const uint32_t blocks = (n + kBlock - 1) / kBlock;
+  hipError_t e = launch_order(len, n, kind.id_prefixed ? 4u : 0u, qws, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tx_blob_kernel, dim3(blocks < grid ? blocks : grid), dim3(kBlock), 0, stream, blobs, off, len,
                      n, msg, sig, pk, txid, status, qws, qws + kQueueHeaderBytes / 4, layout, side, kind);
   return hipGetLastError();
+}
+
+hipError_t launch_tx_blob(const uint8_t* blobs, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* msg,
+                          uint8_t* sig, uint8_t* pk, uint8_t* txid, uint8_t* status, uint32_t* qws, uint32_t grid,
+                          hipStream_t stream, uint32_t kind_id, hipEvent_t parsed) {
+  hipError_t e = launch_tx_blob_parse(blobs, off, len, n, msg, sig, pk, txid, status, qws, grid, stream, kind_id,
+                                      parsed);
+  if (e != hipSuccess) return e;
+  return launch_tx_blob_hash(blobs, off, len, n, msg, sig, pk, txid, status, qws, grid, stream, kind_id);
 }
 
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk, uint8_t* sig, uint4* ws,
