@@ -464,6 +464,10 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
 #define STL_TUNE_R_AHEAD 11          /* 0 / 1 (default 1): a one-call checkSign with a shared key table
                                         decodes every row's R on its own stream beside the key table's
                                         build, and the chunks' phase 1 then only combines the two */
+#define STL_TUNE_FIRST_CHUNK 12      /* 0..2^20, a multiple of 64 (default 0): a device-resident verify over
+                                        several streams starts with a chunk of this many rows (smaller
+                                        than the others): the launch's first phase 1 has no main
+                                        kernel to overlap */
 #define STL_TUNE_RCCL_TIMEOUT_MS 7 /* 1..3,600,000 (default 120,000; env STL_RCCL_TIMEOUT_S): deadline of
                                       stl_comm_init_rank and stl_comm_sync */
 int stl_debug_tuning(int key, int value);

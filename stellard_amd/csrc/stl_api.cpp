@@ -281,6 +281,7 @@ std::atomic<int> g_tune_long_hash{8}; // small batches: rows of more than this m
 std::atomic<int> g_tune_shared_keys{1}; // key dedup over several chunks: one key domain per call (0: one per chunk)
 std::atomic<int> g_tune_wide_min{0};    // key domains of fewer rows build no wide key tables (the 9-entry ones)
 std::atomic<int> g_tune_r_ahead{1};     // one-call checkSign with a shared key domain: R decoded ahead on its own stream
+std::atomic<int> g_tune_first_chunk{0}; // device-resident verify: rows of a smaller first chunk (0: equal chunks)
 
 // Rows per step of verify time: the device-resident verify runs a chunk's
 // 64-signature units on its resident waves, two per SIMD, so its time rises in
@@ -808,6 +809,7 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   x.main_queue = g_tune_queue.load() != 0;
   x.concurrent = concurrent;
   x.sub = chunk_for(d.grid, n);
+  x.first = (uint32_t)g_tune_first_chunk.load();
   uint32_t S = (uint32_t)std::max(1, std::min<int>(streams, (int)stl::kMaxVerifyStreams));
   if (x.clock || n <= x.sub || x.sub <= x.pair_max) S = 1;
   S = (uint32_t)std::min<size_t>(S, (n + x.sub - 1) / x.sub);
@@ -1536,6 +1538,9 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_SHARED_KEYS:
       if (value != 0 && value != 1) return STL_EINVAL;
       return g_tune_shared_keys.exchange(value);
+    case STL_TUNE_FIRST_CHUNK:
+      if (value < 0 || value % 64 != 0 || value > (1 << 20)) return STL_EINVAL;
+      return g_tune_first_chunk.exchange(value);
     case STL_TUNE_R_AHEAD:
       if (value != 0 && value != 1) return STL_EINVAL;
       return g_tune_r_ahead.exchange(value);

@@ -94,6 +94,8 @@ struct VerifyExec {
                                         // two-role phase 1 above pair_max (it trades work for latency)
   uint32_t nstreams = 1;
   uint32_t sub = kPreChunk;             // chunk size when nstreams > 1 (multiple of 64, >= 2^16)
+  uint32_t first = 0;                   // nstreams > 1: a first chunk of this many rows (multiple of 64,
+                                        // < sub), then chunks of `sub`; 0: all of `sub`
   hipStream_t streams[kMaxVerifyStreams] = {};
   uint4* ws[kMaxVerifyStreams] = {};    // verify_ws_bytes(grid, dedup) each
   hipEvent_t fork = nullptr;

@@ -148,10 +148,23 @@ __device__ __forceinline__ void load_k(uint32_t k[8], const uint32_t R[8], const
 // given, PRE_K), lattice reduction of k to half-size (c, d), e = d*S mod L,
 // digits.  Writes quads 0-4 of the lane's HalfState.  Signatures [base,
 // base+cnt).
+// Issue priorities (s_setprio, wave-level arbitration between co-resident
+// waves only): a device-resident checkSign runs its rows' hashing and scalar
+// phase 1 -- the critical path into the main kernels -- beside work with
+// slack (R's decoding ahead, other chunks' main kernels), so these kernels'
+// waves issue first (round 6).
+#ifndef STL_FRONT_PRIO
+#define STL_FRONT_PRIO 2
+#endif
+__device__ __forceinline__ void front_priority() {
+  if (STL_FRONT_PRIO > 0) __builtin_amdgcn_s_setprio(STL_FRONT_PRIO);
+}
+
 template <bool PRE_K>
 __global__ __launch_bounds__(kBlock, STL_SCALAR_WAVES_PER_SIMD) void verify_scalar_kernel(
     const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
     uint32_t base, uint32_t cnt, uint4* __restrict__ pre) {
+  front_priority();
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= cnt) return;  // no wave-level collective in this kernel
   const size_t j = (size_t)base + t;
@@ -1543,6 +1556,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_hash_kerne
                                                          const uint32_t* __restrict__ len, uint32_t n,
                                                          uint8_t* __restrict__ msg, uint32_t* __restrict__ counter,
                                                          const uint32_t* __restrict__ order) {
+  front_priority();
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
@@ -1754,6 +1768,7 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
                                                          const uint32_t* __restrict__ order,
                                                          const uint4* __restrict__ layout,
                                                          const uint4* __restrict__ side, BlobKind kind) {
+  front_priority();
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
@@ -2169,7 +2184,10 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
                 ((uint64_t)n + sub - 1) / sub > (uint64_t)kMainQueueWords))
     S = 1;
   const uint32_t csize = S > 1 ? sub : kPreChunk;
-  const uint64_t nchunks = ((uint64_t)n + csize - 1) / csize;
+  // an optional smaller first chunk (VerifyExec::first): its phase 1 is the
+  // launch's one phase 1 that no main kernel overlaps
+  const uint32_t first = S > 1 && x.first && (x.first & 63u) == 0 && x.first < csize && x.first < n ? x.first : 0u;
+  const uint64_t nchunks = first ? 1 + ((uint64_t)(n - first) + csize - 1) / csize : ((uint64_t)n + csize - 1) / csize;
   if (S > (uint32_t)nchunks) S = (uint32_t)nchunks;
   // points_done covers exactly one lane-pair chunk (launch_verify_points)
   if (x.points_done && (nchunks != 1 || !verify_pair_points(n, policy, x))) return hipErrorInvalidValue;
@@ -2208,8 +2226,9 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   }
   for (uint64_t c = 0; c < nchunks; ++c) {  // 64-bit: n may reach 2^32 - 64
     const uint32_t j = (uint32_t)(c % S);
-    const uint32_t base = (uint32_t)(c * csize);
-    const uint32_t cnt = n - base < csize ? n - base : csize;
+    const uint32_t base = first ? (c == 0 ? 0u : (uint32_t)(first + (c - 1) * csize)) : (uint32_t)(c * csize);
+    const uint32_t cap = first && c == 0 ? first : csize;
+    const uint32_t cnt = n - base < cap ? n - base : cap;
     uint32_t* q = x.main_queue ? queue_counters(x.ws[j], x.grid) + c / S : nullptr;
     if (shared_keys) xk.key_build = c == 0 && !x.key_stream;
     e = verify_chunk(sig, msg_or_k, pk, base, cnt, bitmap, policy, pre_k, xk, x.streams[j], x.ws[j], q,

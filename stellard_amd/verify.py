@@ -606,6 +606,7 @@ TUNE_LONG_HASH = N.STL_TUNE_LONG_HASH
 TUNE_SHARED_KEYS = N.STL_TUNE_SHARED_KEYS
 TUNE_WIDE_MIN_ROWS = N.STL_TUNE_WIDE_MIN_ROWS
 TUNE_R_AHEAD = N.STL_TUNE_R_AHEAD
+TUNE_FIRST_CHUNK = N.STL_TUNE_FIRST_CHUNK
 
 
 def debug_tuning(key, value):
@@ -681,7 +682,7 @@ def execution_settings():
         ("fused_prep", TUNE_FUSED_PREP), ("main_queue", TUNE_MAIN_QUEUE), ("streams", TUNE_STREAMS),
         ("chunk_log2", TUNE_CHUNK_LOG2), ("quad", TUNE_QUAD), ("long_hash", TUNE_LONG_HASH),
         ("shared_keys", TUNE_SHARED_KEYS), ("wide_min_rows", TUNE_WIDE_MIN_ROWS),
-        ("r_ahead", TUNE_R_AHEAD))}
+        ("r_ahead", TUNE_R_AHEAD), ("first_chunk", TUNE_FIRST_CHUNK))}
 
 
 def sign_batch_device(seed, msg, stream=None):

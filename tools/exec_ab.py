@@ -7,7 +7,7 @@ measurement (as bench.py's timed region), settings interleaved in rotating
 order over R repetitions; median ms per launch.  Every setting's bitmap must
 equal the first setting's.
 
-    python tools/exec_ab.py [K] [R] [name=fused,queue,streams,log2 ...]
+    python tools/exec_ab.py [K] [R] [name=fused,queue,streams,log2[,first] ...]
 """
 import json
 import os
@@ -50,6 +50,7 @@ def main():
         V.debug_tuning(V.TUNE_MAIN_QUEUE, v[1])
         V.debug_tuning(V.TUNE_STREAMS, v[2])
         V.debug_tuning(V.TUNE_CHUNK_LOG2, v[3])
+        V.debug_tuning(V.TUNE_FIRST_CHUNK, v[4] if len(v) > 4 else 0)  # rows of a smaller first chunk
 
     ref = None
     for name, v in cfgs:  # warm-up and parity
