@@ -148,23 +148,10 @@ __device__ __forceinline__ void load_k(uint32_t k[8], const uint32_t R[8], const
 // given, PRE_K), lattice reduction of k to half-size (c, d), e = d*S mod L,
 // digits.  Writes quads 0-4 of the lane's HalfState.  Signatures [base,
 // base+cnt).
-// Issue priorities (s_setprio, wave-level arbitration between co-resident
-// waves only): a device-resident checkSign runs its rows' hashing and scalar
-// phase 1 -- the critical path into the main kernels -- beside work with
-// slack (R's decoding ahead, other chunks' main kernels), so these kernels'
-// waves issue first (round 6).
-#ifndef STL_FRONT_PRIO
-#define STL_FRONT_PRIO 2
-#endif
-__device__ __forceinline__ void front_priority() {
-  if (STL_FRONT_PRIO > 0) __builtin_amdgcn_s_setprio(STL_FRONT_PRIO);
-}
-
 template <bool PRE_K>
 __global__ __launch_bounds__(kBlock, STL_SCALAR_WAVES_PER_SIMD) void verify_scalar_kernel(
     const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg_or_k, const uint8_t* __restrict__ pk,
     uint32_t base, uint32_t cnt, uint4* __restrict__ pre) {
-  front_priority();
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= cnt) return;  // no wave-level collective in this kernel
   const size_t j = (size_t)base + t;
@@ -1556,7 +1543,6 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_hash_kerne
                                                          const uint32_t* __restrict__ len, uint32_t n,
                                                          uint8_t* __restrict__ msg, uint32_t* __restrict__ counter,
                                                          const uint32_t* __restrict__ order) {
-  front_priority();
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
@@ -1768,7 +1754,6 @@ __global__ __launch_bounds__(kBlock, STL_HASH_WAVES_PER_SIMD) void tx_blob_kerne
                                                          const uint32_t* __restrict__ order,
                                                          const uint4* __restrict__ layout,
                                                          const uint4* __restrict__ side, BlobKind kind) {
-  front_priority();
   __shared__ uint4 win_all[kBlock / 64][64 * kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* win = win_all[threadIdx.x >> 6];
@@ -2210,7 +2195,8 @@ hipError_t launch_verify(const uint8_t* sig, const uint8_t* msg_or_k, const uint
   // built by chunk 0 on streams[0] right after its scalar kernel
   VerifyExec xk = x;
   const bool shared_keys = (policy & kModeDedupKeys) && nchunks > 1 && n <= kPreChunk && x.key_ready &&
-                           !x.key_ws && csize > x.pair_max;  // chunk 0 runs the one-lane path that builds it
+                           !x.key_ws && csize > x.pair_max &&  // chunk 0 runs the one-lane path that builds it
+                           (first == 0 || first > x.pair_max);
   if (shared_keys) {
     xk.key_ws = x.ws[0];
     xk.key_base = 0;

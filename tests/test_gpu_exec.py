@@ -26,16 +26,19 @@ def stl(torch_cuda):
     return verify
 
 
-SETTINGS = [  # (fused_prep, main_queue, streams, chunk_log2)
+SETTINGS = [  # (fused_prep, main_queue, streams, chunk_log2[, first chunk rows])
     (0, 0, 1, 18), (1, 0, 1, 18), (0, 1, 1, 18), (1, 1, 1, 18),
     (1, 1, 2, 18), (1, 1, 4, 18), (1, 1, 3, 17), (1, 1, 4, 16), (0, 0, 2, 19), (1, 1, 2, 20), (1, 1, 2, 0),
     (1, 1, 2, 15), (1, 1, 3, 15),  # lane-pair chunks on concurrent streams
+    (1, 1, 2, 0, 65536), (1, 1, 2, 0, 32768), (1, 1, 3, 17, 100032),  # a smaller first chunk (STL_TUNE_FIRST_CHUNK)
 ]
 
 
 def _apply(stl, v):
     old = []
-    for key, val in zip((stl.TUNE_FUSED_PREP, stl.TUNE_MAIN_QUEUE, stl.TUNE_STREAMS, stl.TUNE_CHUNK_LOG2), v):
+    v = tuple(v) + (0,) * (5 - len(v))
+    for key, val in zip((stl.TUNE_FUSED_PREP, stl.TUNE_MAIN_QUEUE, stl.TUNE_STREAMS, stl.TUNE_CHUNK_LOG2,
+                         stl.TUNE_FIRST_CHUNK), v):
         old.append(stl.debug_tuning(key, val))
     return tuple(old)
 
@@ -97,7 +100,7 @@ def test_settings_same_bits_with_flags(stl, torch_cuda, batch, flags):
     old = _apply(stl, SETTINGS[0])
     try:
         ref = _run(stl, torch, d, n, pol)
-        for v in ((1, 1, 1, 18), (1, 1, 4, 16), (1, 1, 2, 18), (0, 1, 2, 17)):
+        for v in ((1, 1, 1, 18), (1, 1, 4, 16), (1, 1, 2, 18), (0, 1, 2, 17), (1, 1, 2, 0, 65536)):
             _apply(stl, v)
             assert np.array_equal(_run(stl, torch, d, n, pol), ref), (flags, v)
     finally:
