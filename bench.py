@@ -301,8 +301,11 @@ def config1_leg(V, torch, dev, stream, threads_share):
         return V.signed_blob_verify_batch_device(d_buf, d_off, d_len, out_words=words, out_status=status,
                                                  stream=stream)
 
-    def med(fn, reps=7):
-        fn()
+    def med(fn, reps=15, warm=3):
+        # warm calls: the device sat idle while the host legs ran, and the
+        # first calls of a stream also settle its automatic-dedup verdict
+        for _ in range(warm):
+            fn()
         torch.cuda.synchronize()
         ts = []
         for _ in range(reps):

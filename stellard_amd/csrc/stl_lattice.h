@@ -249,9 +249,12 @@ STL_HD void lat_madd2(uint32_t out[5], uint32_t ua, const uint32_t A[5], uint32_
 // Y = det*(m00 rs - m10 rl), det = (-1)^steps.  Truncating to the leading
 // parts leaves |X/2^sh - x| < max(m11, m01) =: M1 and |Y/2^sh - y| < M2 :=
 // max(m10, m00), so q = floor(x / y), r = x - q y is the true quotient of
-// (X, Y) when  r >= M1 + q M2  and  y - r >= M1 + (q + 1) M2;  the step is
-// also taken only while the new remainder is certainly >= 2^128 (the exact
-// Euclid's stopping rule) and the matrix stays below 2^32.
+// (X, Y) when  r >= M1 + q M2  and  y - r >= M1 + (q + 1) M2,  and the step
+// is taken while the matrix stays below 2^32.  Euclid stops at the first
+// remainder below 2^128: the round goes on only while the new remainder is
+// certainly >= 2^128, and otherwise ends with the step that may have crossed
+// (lattice_half tests the rows exactly), so a lane's last step is a certified
+// one too instead of a round of its own through lat_step.
 // At most kLehmerSteps certified steps per round: a wave runs each round's
 // loop to its slowest lane, and lanes certify 8-30 quotients from 53 bits
 // (tools/lattice_sim.cpp, 2,000 waves of random k: 121.6 iterations in 7.03
@@ -284,7 +287,7 @@ STL_HD void lat_lehmer_round(uint32_t rl[8], uint32_t rs[8], uint32_t tl[5], uin
     const double n00 = fma(m00, q, m01), n10 = fma(m10, q, m11);
     const double M2n = fmax(n00, n10);
     const bool step = y > 0.0 && r >= 0.0 && r < y && r >= fma(q, M2, M1) && y - r >= fma(q + 1.0, M2, M1) &&
-                      M2n < 4294967296.0 && r - M2n >= thr;
+                      M2n < 4294967296.0;
     go = go && step;
     if (go) {
       m01 = m00;
@@ -295,6 +298,9 @@ STL_HD void lat_lehmer_round(uint32_t rl[8], uint32_t rs[8], uint32_t tl[5], uin
       y = r;
       odd = !odd;
     }
+    // the new remainder may be below 2^128: the round ends with this step,
+    // and the caller's exact test decides whether another round follows
+    go = go && r - M2n >= thr;
   }
   if (!act) return;
   if (m10 != 0.0) {  // at least one certified step: apply M

@@ -28,9 +28,10 @@ static int round_count(uint32_t rl[8], uint32_t rs[8], uint32_t tl[5], uint32_t 
     const double n00 = fma(m00, q, m01), n10 = fma(m10, q, m11);
     const double M2n = fmax(n00, n10);
     const bool step = y > 0.0 && r >= 0.0 && r < y && r >= fma(q, M2, M1) && y - r >= fma(q + 1.0, M2, M1) &&
-                      M2n < 4294967296.0 && r - M2n >= thr;
+                      M2n < 4294967296.0;
     if (!step) break;
     m01 = m00; m00 = n00; m11 = m10; m10 = n10; x = y; y = r; odd = !odd;
+    if (r - M2n < thr) break;
   }
   if (m10 != 0.0) {
     const uint32_t u00 = (uint32_t)m00, u01 = (uint32_t)m01, u10 = (uint32_t)m10, u11 = (uint32_t)m11;
