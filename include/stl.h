@@ -468,9 +468,6 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
                                         several streams starts with a chunk of this many rows (smaller
                                         than the others): the launch's first phase 1 has no main
                                         kernel to overlap */
-#define STL_TUNE_TAIL_PAIRS 13       /* 0..32,768 (default 0): a call of n rows with 3 * P < n <= 3 * P + this
-                                        (P = the lane-pair chunk size, 32,768 on 256 CUs) runs a 2 * P
-                                        one-lane chunk and its remainder on lane pairs */
 #define STL_TUNE_RCCL_TIMEOUT_MS 7 /* 1..3,600,000 (default 120,000; env STL_RCCL_TIMEOUT_S): deadline of
                                       stl_comm_init_rank and stl_comm_sync */
 int stl_debug_tuning(int key, int value);

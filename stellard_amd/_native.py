@@ -49,7 +49,6 @@ STL_TUNE_SHARED_KEYS = 9
 STL_TUNE_WIDE_MIN_ROWS = 10
 STL_TUNE_R_AHEAD = 11
 STL_TUNE_FIRST_CHUNK = 12
-STL_TUNE_TAIL_PAIRS = 13
 
 # per-transaction status of the serialized-transaction entry points
 STL_TX_OK = 0

@@ -282,7 +282,6 @@ std::atomic<int> g_tune_shared_keys{1}; // key dedup over several chunks: one ke
 std::atomic<int> g_tune_wide_min{0};    // key domains of fewer rows build no wide key tables (the 9-entry ones)
 std::atomic<int> g_tune_r_ahead{1};     // one-call checkSign with a shared key domain: R decoded ahead on its own stream
 std::atomic<int> g_tune_first_chunk{0}; // device-resident verify: rows of a smaller first chunk (0: equal chunks)
-std::atomic<int> g_tune_tail_pairs{0};  // rows a lane-pair remainder chunk may run above pair_max (0: none)
 
 // Rows per step of verify time: the device-resident verify runs a chunk's
 // 64-signature units on its resident waves, two per SIMD, so its time rises in
@@ -306,7 +305,7 @@ uint32_t chunk_for(uint32_t grid, size_t n) {
   // three: 2 * pair_max and a lane-pair remainder (98,304: 1.01 vs 1.05 ms)
   const size_t pm = pair_max_lanes(grid);
   if (n <= 2 * pm) return (uint32_t)std::min<size_t>(std::max<size_t>(n, 64), stl::kPreChunk);
-  if (n <= 3 * pm + (size_t)g_tune_tail_pairs.load()) return (uint32_t)(2 * pm);
+  if (n <= 3 * pm) return (uint32_t)(2 * pm);
   const size_t nc = std::max<size_t>(2, (n + ((size_t)1 << 17)) >> 18);
   size_t sub = ((n + nc - 1) / nc + 63) / 64 * 64;
   sub = std::max<size_t>(sub, pair_max_lanes(grid) + 64);
@@ -765,15 +764,6 @@ uint32_t verify_grid_for(const Device& d, size_t n) {
 // per SIMD at most (a quarter of the resident lanes).
 uint32_t pair_max_lanes(uint32_t grid) { return grid * stl::kBlock / 4; }
 uint32_t pair_max(const Device& d) { return pair_max_lanes(d.grid); }
-// The lane-pair cap of a launch of n rows: pair_max, or -- with
-// STL_TUNE_TAIL_PAIRS and n a little past three lane-pair chunks -- the
-// remainder after chunk_for's 2 * pair_max chunk, so that it runs on lane
-// pairs too (at most two pair waves on some SIMDs).
-uint32_t pair_cap(const Device& d, size_t n) {
-  const size_t pm = pair_max(d);
-  const size_t tail = (size_t)g_tune_tail_pairs.load();
-  return n > 3 * pm && n <= 3 * pm + tail ? (uint32_t)(n - 2 * pm) : (uint32_t)pm;
-}
 // Largest chunks whose main kernel runs on eight (quad_max) or four (duo_max)
 // lanes per signature: one such wave per SIMD at most (a second one per SIMD
 // measured slower than lane pairs; STL_TUNE_QUAD bits 0 / 1 turn them on).
@@ -809,7 +799,7 @@ int run_verify(Device& d, hipStream_t s, const uint8_t* sig, const uint8_t* msg_
   stl::VerifyExec x;
   x.grid = verify_grid_for(d, n);
   x.ws_grid = d.grid;  // every workspace is verify_ws_bytes(d.grid, ...)
-  x.pair_max = pair_cap(d, n);
+  x.pair_max = pair_max(d);
   x.quad_max = quad_max(d);
   x.duo_max = duo_max(d);
   x.wide = static_cast<const uint4*>(d.wide.p);
@@ -1551,9 +1541,6 @@ int stl_debug_tuning(int key, int value) {
     case STL_TUNE_FIRST_CHUNK:
       if (value < 0 || value % 64 != 0 || value > (1 << 20)) return STL_EINVAL;
       return g_tune_first_chunk.exchange(value);
-    case STL_TUNE_TAIL_PAIRS:
-      if (value < 0 || value > (int)stl::kPreChunk / 32) return STL_EINVAL;
-      return g_tune_tail_pairs.exchange(value);
     case STL_TUNE_R_AHEAD:
       if (value != 0 && value != 1) return STL_EINVAL;
       return g_tune_r_ahead.exchange(value);
@@ -1866,7 +1853,7 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
     stl::VerifyExec x;
     x.grid = verify_grid_for(d, cnt);
     x.ws_grid = d.grid;  // every workspace is verify_ws_bytes(d.grid, ...)
-    x.pair_max = pair_cap(d, n);
+    x.pair_max = pair_max(d);
     x.quad_max = quad_max(d);
     x.duo_max = duo_max(d);
     x.wide = static_cast<const uint4*>(d.wide.p);
@@ -2013,7 +2000,13 @@ int checksign_device(Device& d, hipStream_t s, bool blob, uint32_t kind, const u
       e = hipStreamWaitEvent(cr, c.fork, 0);
     }
     if (e == hipSuccess && fault_now()) e = hipErrorUnknown;
-    if (e == hipSuccess) e = stl::launch_point_r(sig, pk, (uint32_t)n, mode, static_cast<uint4*>(c.rdec.p), cr);
+    // a last chunk on lane pairs decodes R in its own pair kernel: only the
+    // one-lane chunks' rows are decoded ahead
+    const size_t last = n - (n - 1) / sub * sub;
+    const bool last_pairs = n > sub && !(mode & stl::kModeOneLane) && last <= pair_max(d);
+    const size_t r_rows = last_pairs ? n - last : n;
+    if (e == hipSuccess)
+      e = stl::launch_point_r(sig, pk, (uint32_t)r_rows, mode, static_cast<uint4*>(c.rdec.p), cr);
     if (e == hipSuccess) e = hipEventRecord(c.rready, cr);
     if (e != hipSuccess) return fail(STL_EHIP);
   }

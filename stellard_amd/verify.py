@@ -607,7 +607,6 @@ TUNE_SHARED_KEYS = N.STL_TUNE_SHARED_KEYS
 TUNE_WIDE_MIN_ROWS = N.STL_TUNE_WIDE_MIN_ROWS
 TUNE_R_AHEAD = N.STL_TUNE_R_AHEAD
 TUNE_FIRST_CHUNK = N.STL_TUNE_FIRST_CHUNK
-TUNE_TAIL_PAIRS = N.STL_TUNE_TAIL_PAIRS
 
 
 def debug_tuning(key, value):
@@ -683,8 +682,7 @@ def execution_settings():
         ("fused_prep", TUNE_FUSED_PREP), ("main_queue", TUNE_MAIN_QUEUE), ("streams", TUNE_STREAMS),
         ("chunk_log2", TUNE_CHUNK_LOG2), ("quad", TUNE_QUAD), ("long_hash", TUNE_LONG_HASH),
         ("shared_keys", TUNE_SHARED_KEYS), ("wide_min_rows", TUNE_WIDE_MIN_ROWS),
-        ("r_ahead", TUNE_R_AHEAD), ("first_chunk", TUNE_FIRST_CHUNK),
-        ("tail_pairs", TUNE_TAIL_PAIRS))}
+        ("r_ahead", TUNE_R_AHEAD), ("first_chunk", TUNE_FIRST_CHUNK))}
 
 
 def sign_batch_device(seed, msg, stream=None):

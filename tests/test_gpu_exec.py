@@ -251,26 +251,3 @@ def test_overlap_survives_caller_streams(stl, torch_cuda):
     finally:
         _apply(stl, old)
 
-
-@pytest.mark.parametrize("policy", ["default", "dedup"])
-def test_tail_pairs_same_bits(stl, torch_cuda, batch, policy):
-    """STL_TUNE_TAIL_PAIRS: a call a little past three lane-pair chunks' rows
-    runs a 2 * pair_max one-lane chunk and its remainder on lane pairs (more
-    than one pair wave on some SIMDs); the bits must not change, for plain and
-    key-dedup launches, at sizes inside and outside the knob's window."""
-    torch = torch_cuda
-    n, d, host, rows, exp_golden, flip = batch
-    pol = stl.DEDUP_KEYS if policy == "dedup" else 0
-    old = _apply(stl, (1, 1, 2, 0))
-    prev = stl.debug_tuning(stl.TUNE_TAIL_PAIRS, 0)
-    try:
-        for m in (98_304, 100_000, 110_017, 131_072):
-            dm = [a[:m] for a in d]
-            ref = _run(stl, torch, dm, m, pol)
-            stl.debug_tuning(stl.TUNE_TAIL_PAIRS, 32_768)
-            got = _run(stl, torch, dm, m, pol)
-            stl.debug_tuning(stl.TUNE_TAIL_PAIRS, 0)
-            assert np.array_equal(got, ref), (m, np.nonzero(got != ref)[0][:8])
-    finally:
-        stl.debug_tuning(stl.TUNE_TAIL_PAIRS, prev)
-        _apply(stl, old)

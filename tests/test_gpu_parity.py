@@ -607,8 +607,10 @@ def test_shared_key_domain_same_bits(stl, golden, oracle, torch_cuda, policy):
         assert np.array_equal(got[1][samp], oracle.verify_batch(s_np[samp], m_np[samp], p_np[samp], policy=policy))
     # one-call checkSign over preimages, 2 chunks, forced dedup, shared vs not;
     # 99,968 rows: chunks of 50,048 and 49,920 rows whose verify grids differ
-    # (196 vs 195 workgroups' worth) while they share one key domain
-    for n in (150_000, 99_968):
+    # (196 vs 195 workgroups' worth) while they share one key domain;
+    # 90,000 rows: a 65,536-row one-lane chunk and a lane-pair remainder,
+    # which decodes its own R (only the first chunk's rows are decoded ahead)
+    for n in (150_000, 99_968, 90_000):
         _one_call_shared_keys(stl, torch, rng, n, policy)
 
 
