@@ -1451,13 +1451,43 @@ __global__ __launch_bounds__(kBlock) void order_scatter_kernel(const uint32_t* _
   }
 }
 
+// The long row's 80 rounds on lane pairs (stl_sha512.h pair_round_front /
+// _back) and the feed-forward: this lane's four state words s4, the
+// partner's word by one DPP swap, W[t] + K[t] = get(t) read kAhead rounds
+// ahead of its use (a ring in registers, each read pinned behind round
+// t - kAhead's state, so the compiler neither hoists all 80 reads nor leaves
+// a read's latency inside the chain).  Round 6: 36 instructions per round
+// against 41 for the whole round on every lane (the previous form), a
+// 4-KB row's hash 12 % faster (DESIGN_EXPERIMENTS.md).
+template <typename Get>
+__device__ __forceinline__ void sha512_rounds_pair(W64 s4[4], const PairSide& ps, const Get& get) {
+  constexpr int kAhead = 8;
+  W64 r[4] = {s4[0], s4[1], s4[2], s4[3]};
+  W64 ring[kAhead];
+#pragma unroll
+  for (int i = 0; i < kAhead; ++i) ring[i] = get(i);
+#pragma clang loop unroll(full)
+  for (int i = 0; i < 80; ++i) {
+    const W64 kw = ring[i % kAhead];
+    if (i + kAhead < 80) {
+      asm volatile("" : "+v"(r[0].lo)::"memory");
+      ring[i % kAhead] = get(i + kAhead);
+    }
+    W64 T, U;
+    pair_round_front<true>(r, kw, ps, T, U);
+    pair_round_back<true>(r, T, W64{pair_swap(U.lo), pair_swap(U.hi)});
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s4[j] = add64(s4[j], r[j]);
+}
+
 // tx_hash_kernel's long mode (small batches: the longest row sets the
 // call's latency): the first K = counter[2] rows of the order, one per wave.
 // Lanes 0..kLongBatch-1 each load one block of the row (a 144-byte window of
 // 16-byte loads, as wave_window_fill takes them) and expand its schedule into
 // the wave's window area; the wave then runs the rounds block after block
-// reading W[t] from LDS (a broadcast read), so the schedule leaves the
-// dependent chain.
+// on lane pairs (sha512_rounds_pair) reading W[t] from LDS (a broadcast
+// read), so the schedule leaves the dependent chain.
 __device__ __forceinline__ void hash_long_rows(const uint8_t* __restrict__ pre, const uint64_t* __restrict__ off,
                                                const uint32_t* __restrict__ len, uint8_t* __restrict__ msg,
                                                uint32_t* __restrict__ counter, const uint32_t* __restrict__ order,
@@ -1484,6 +1514,11 @@ __device__ __forceinline__ void hash_long_rows(const uint8_t* __restrict__ pre, 
     const uint32_t nbl = (L + 17u + 127u) >> 7;
     uint64_t st[8];
     sha512_init(st);
+    // lane pairs: the odd lanes keep H0..H3 (a..d), the even lanes H4..H7
+    const PairSide ps = pair_side((lane & 1u) != 0);
+    W64 s4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s4[j] = w64(st[(ps.a_side ? 0 : 4) + j]);
     for (uint32_t b0 = 0; b0 < nbl; b0 += kLongBatch) {
       const uint32_t cnt = nbl - b0 < kLongBatch ? nbl - b0 : kLongBatch;
       if (lane < cnt) {
@@ -1513,20 +1548,21 @@ __device__ __forceinline__ void hash_long_rows(const uint8_t* __restrict__ pre, 
       asm volatile("" ::: "memory");
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint2* src = wsch + 80u * j;
-        sha512_rounds<true, true>(st, [&](int t) {
+        auto get = [&](int t) {
           const uint2 v = src[t];
           return W64{v.x, v.y};
-        });
+        };
+        sha512_rounds_pair(s4, ps, get);
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
     }
-    if (lane == 0) {
+    if (lane == 1u) {  // an a-side lane: H0..H3, the signing hash
       uint32_t h[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        h[2 * j] = bswap32((uint32_t)(st[j] >> 32));
-        h[2 * j + 1] = bswap32((uint32_t)st[j]);
+        h[2 * j] = bswap32(s4[j].hi);
+        h[2 * j + 1] = bswap32(s4[j].lo);
       }
       st8(msg + 32 * (size_t)row, h);
     }

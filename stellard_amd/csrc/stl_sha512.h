@@ -194,38 +194,58 @@ STL_HD void sha512_schedule(const uint64_t win[16], Put put) {
 // through an SGPR, so no hazard nop -- the lone-wave latency path's add
 STL_HD W64 add64(W64 a, W64 b) { return w64(u64(a) + u64(b)); }
 
-// 80 rounds + feed-forward with W[t] = get(t), read kAhead rounds ahead of
-// their use (a ring in registers): the reads are pinned behind round
-// t - kAhead's state so the compiler neither hoists all 80 (160 VGPRs) nor
-// leaves a read's latency inside the chain.
-// With KW, get(t) returns W[t] + K[t] (the caller folded the round constant
-// into the schedule, off the rounds' chain).
-template <bool ADD64 = false, bool KW = false, typename Get>
-STL_HD void sha512_rounds(uint64_t st[8], const Get& get) {
-  constexpr int kAhead = 8;
-  auto ad = [](W64 x, W64 y) { return ADD64 ? add64(x, y) : add(x, y); };
-  W64 a = w64(st[0]), b = w64(st[1]), c = w64(st[2]), d = w64(st[3]);
-  W64 e = w64(st[4]), f = w64(st[5]), g = w64(st[6]), h = w64(st[7]);
-  W64 ring[kAhead];
-#pragma unroll
-  for (int i = 0; i < kAhead; ++i) ring[i] = get(i);
-#pragma clang loop unroll(full)
-  for (int i = 0; i < 80; ++i) {
-    const W64 wi = ring[i % kAhead];
-    if (i + kAhead < 80) {
-#if defined(__HIP_DEVICE_COMPILE__)
-      asm volatile("" : "+v"(a.lo), "+v"(e.lo)::"memory");
-#endif
-      ring[i % kAhead] = get(i + kAhead);
-    }
-    const W64 S1 = xor3(rotr<14>(e), rotr<18>(e), rotr<41>(e));
-    const W64 t1 = KW ? ad(ad(h, S1), ad(ch(e, f, g), wi)) : ad(ad(h, S1), ad(ad(ch(e, f, g), sha_kw(i)), wi));
-    const W64 S0 = xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a));
-    const W64 t2 = ad(S0, maj(a, b, c));
-    h = g; g = f; f = e; e = ad(d, t1); d = c; c = b; b = a; a = ad(t1, t2);
-  }
-  st[0] += u64(a); st[1] += u64(b); st[2] += u64(c); st[3] += u64(d);
-  st[4] += u64(e); st[5] += u64(f); st[6] += u64(g); st[7] += u64(h);
+// ---- the rounds on a lane pair (one long row: the latency path) ----
+// A round's two halves are one instruction stream with per-lane operands.
+// The e-side lane keeps (e, f, g, h) and makes T1 = h + S1(e) + Ch(e, f, g)
+// + K + W; the a-side lane keeps (a, b, c, d) and makes T2 = S0(a) +
+// Maj(a, b, c).  S1 and S0 are three rotations and a xor3 each, with
+// per-lane amounts (one of S0's is >= 32 where S1's is not: that lane
+// rotates its word with the halves swapped); Maj(a, b, c) = (~(a ^ b)) ? b
+// : c, so both lanes run Ch(x, y, z) = x ? y : z with x = e or ~(a ^ b)
+// (one bitop3 per half on a lane mask).  Then each lane adds the value its
+// partner sends -- d to the e-side (e' = d + T1), T1 to the a-side (a' = T1
+// + T2) -- and shifts its four words.  ≈28 instructions per round for the
+// pair against ≈40 for the whole round on one lane.
+struct PairSide {
+  uint32_t s1, s2, s3;  // alignbit amounts of the three rotations
+  uint32_t am;          // ~0 on the a-side, 0 on the e-side
+  bool a_side;
+};
+
+STL_HD PairSide pair_side(bool a_side) {
+  // S1: rotr 14, 18, 41 (the last as 32 + 9); S0: rotr 28, 34 (32 + 2, on the
+  // swapped word), 39 (32 + 7)
+  return a_side ? PairSide{28u, 2u, 7u, ~0u, true} : PairSide{14u, 18u, 9u, 0u, false};
+}
+
+// front half: T (T1 on the e-side, T2 on the a-side) and U, the word the
+// partner lane needs (the e-side sends T1, the a-side sends d)
+template <bool ADD64 = true>
+STL_HD void pair_round_front(const W64 r[4], W64 kw, const PairSide& ps, W64& T, W64& U) {
+  auto ad = [](W64 a, W64 b) { return ADD64 ? add64(a, b) : add(a, b); };
+  const W64 x = r[0];
+  const W64 xs = ps.a_side ? W64{x.hi, x.lo} : x;
+  const W64 r1{abit(x.hi, x.lo, ps.s1), abit(x.lo, x.hi, ps.s1)};
+  const W64 r2{abit(xs.hi, xs.lo, ps.s2), abit(xs.lo, xs.hi, ps.s2)};
+  const W64 r3{abit(x.lo, x.hi, ps.s3), abit(x.hi, x.lo, ps.s3)};
+  const W64 S = xor3(r1, r2, r3);
+  // x' = x ^ (am & ~y): e on the e-side, ~(a ^ b) on the a-side
+  const W64 xp{bitop3<0xD2u>(x.lo, r[1].lo, ps.am), bitop3<0xD2u>(x.hi, r[1].hi, ps.am)};
+  const W64 C = ch(xp, r[1], r[2]);
+  W64 P = ad(r[3], kw);  // h + K + W, the e-side's only
+  P.lo &= ~ps.am;
+  P.hi &= ~ps.am;
+  T = ad(ad(S, C), P);
+  U = ps.a_side ? r[3] : T;
+}
+
+// back half: the partner's word added, the four words shifted
+template <bool ADD64 = true>
+STL_HD void pair_round_back(W64 r[4], W64 T, W64 Up) {
+  r[3] = r[2];
+  r[2] = r[1];
+  r[1] = r[0];
+  r[0] = ADD64 ? add64(T, Up) : add(T, Up);
 }
 
 STL_HD uint32_t bswap32(uint32_t x) {

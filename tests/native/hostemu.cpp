@@ -281,6 +281,35 @@ void hostemu_sha512_half(const uint8_t* p, uint32_t len, uint8_t out[32]) {
   std::memcpy(out, o, 32);
 }
 
+// One SHA-512 compression as the long-row kernel runs it on a lane pair
+// (stl_sha512.h pair_round_front / _back), both lanes emulated in lockstep:
+// st[8] (H0..H7) updated by the block w[16] (big-endian 64-bit words).
+void hostemu_sha512_pair_compress(uint64_t st[8], const uint64_t w[16], int add64) {
+  uint64_t sched[80];
+  stl::sha512_schedule(w, [&](int t, stl::W64 v) { sched[t] = stl::u64(v); });
+  stl::W64 r[2][4];
+  for (int j = 0; j < 4; ++j) {
+    r[0][j] = stl::w64(st[4 + j]);  // e-side lane: e, f, g, h
+    r[1][j] = stl::w64(st[j]);      // a-side lane: a, b, c, d
+  }
+  const stl::PairSide ps[2] = {stl::pair_side(false), stl::pair_side(true)};
+  for (int t = 0; t < 80; ++t) {
+    const stl::W64 kw = stl::w64(sched[t] + stl::sha_k(t));
+    stl::W64 T[2], U[2];
+    for (int l = 0; l < 2; ++l) {
+      if (add64)
+        stl::pair_round_front<true>(r[l], kw, ps[l], T[l], U[l]);
+      else
+        stl::pair_round_front<false>(r[l], kw, ps[l], T[l], U[l]);
+    }
+    for (int l = 0; l < 2; ++l) stl::pair_round_back(r[l], T[l], U[1 - l]);
+  }
+  for (int j = 0; j < 4; ++j) {
+    st[4 + j] += stl::u64(r[0][j]);
+    st[j] += stl::u64(r[1][j]);
+  }
+}
+
 // The device's serialized-transaction pass (stl_txblob.h) for one blob:
 // status, signing hash (splice), transaction ID, and the layout numbers
 // (pk_off, pk_len, sig_off, sig_len, xs0, xe0, xs1, xe1, xs2, xe2).

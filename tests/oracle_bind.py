@@ -282,6 +282,7 @@ def load_hostemu():
     lib.hostemu_lattice.argtypes = [V, V, V, V]
     lib.hostemu_sc_mul_signed.argtypes = [V, ctypes.c_int, V, V]
     lib.hostemu_sha512_half.argtypes = [V, ctypes.c_uint32, V]
+    lib.hostemu_sha512_pair_compress.argtypes = [V, V, ctypes.c_int]
     lib.hostemu_tx_blob.argtypes = [V, ctypes.c_uint32, V, V, V, V]
     lib.hostemu_signed_blob.argtypes = [ctypes.c_uint32, V, ctypes.c_uint32, V, V, V]
     lib.hostemu_blob_words.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, V]

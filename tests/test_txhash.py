@@ -61,3 +61,25 @@ def test_block_from_window_matches_bytestream():
         for ln in (0, 1, 3, 4, 5, 107, 108, 111, 112, 113, 127, 128, 129, 240, 256, 1000, 4100):
             assert emu.hostemu_window_blocks(buf.ctypes.data_as(ctypes.c_void_p), off, ln, 0, 0) == 0, (off, ln)
             assert emu.hostemu_window_blocks(buf.ctypes.data_as(ctypes.c_void_p), off, ln, 0x004E5854, 1) == 0, (off, ln)
+
+
+def test_pair_rounds_equal_sha512(emu):
+    """The long-row kernel's lane-pair rounds (stl_sha512.h pair_round_front /
+    pair_round_back, both lanes emulated on the host): chaining the pair
+    compression over padded messages gives hashlib's SHA-512, for lengths
+    that cross block boundaries."""
+    rng = np.random.default_rng(31)
+    iv = [0x6a09e667f3bcc908, 0xbb67ae8584caa73b, 0x3c6ef372fe94f82b, 0xa54ff53a5f1d36f1,
+          0x510e527fade682d1, 0x9b05688c2b3e6c1f, 0x1f83d9abfb41bd6b, 0x5be0cd19137e2179]
+    for n in (0, 1, 111, 112, 127, 128, 239, 240, 1000, 4096):
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        pad = m + b"\x80" + b"\x00" * ((111 - n) % 128) + (8 * n).to_bytes(16, "big")
+        assert len(pad) % 128 == 0
+        for add64 in (1, 0):
+            st = np.array(iv, dtype=np.uint64)
+            for b in range(0, len(pad), 128):
+                w = np.array([int.from_bytes(pad[b + 8 * j:b + 8 * j + 8], "big") for j in range(16)],
+                             dtype=np.uint64)
+                emu.hostemu_sha512_pair_compress(st.ctypes.data, w.ctypes.data, add64)
+            got = b"".join(int(x).to_bytes(8, "big") for x in st)
+            assert got == hashlib.sha512(m).digest(), (n, add64)
