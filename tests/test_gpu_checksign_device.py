@@ -123,7 +123,9 @@ def test_signed_blob_verify_device_equals_two_step(stl, torch_cuda):
     d_off = torch.from_numpy(offs.view(np.int64)).cuda()
     d_len = torch.from_numpy(lens.view(np.int32)).cuda()
     for kind in (0, 1):  # STL_BLOB_TRANSACTION, STL_BLOB_VALIDATION
-        for m in (n, 65_536, 1_000, 100_001):
+        # 90,000: a 65,536-row one-lane chunk and a lane-pair remainder (whose R
+        # is not decoded ahead) under the automatic dedup of the earlier calls
+        for m in (n, 65_536, 1_000, 100_001, 90_000):
             sl = slice(0, m)
             o = stl.tx_blob_prepare_device(d_buf, d_off[sl], d_len[sl], tx_ids=True, kind=kind)
             two = stl.verify_batch_device(o["sig"], o["msg"], o["pk"])
