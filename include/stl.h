@@ -444,7 +444,7 @@ int stl_debug_verify_k_device(const uint8_t *d_sig, const uint8_t *d_k, const ui
                                   quads (each group formula's four products one per lane), 2 = the
                                   next ones up to one wave per SIMD at four lanes on lane duos (two
                                   products per lane); 3 (default) both, 0 lane pairs only */
-#define STL_TUNE_STREAM_WORKSPACES 6 /* 1..64 (default 4, env STL_MAX_STREAM_WORKSPACES): caller streams
+#define STL_TUNE_STREAM_WORKSPACES 6 /* 1..64 (default 8, env STL_MAX_STREAM_WORKSPACES): caller streams
                                         per device whose context (verify workspace ~0.44 GB, hash
                                         queue, checkSign scratch) libstl keeps; the least recently
                                         used one beyond it is evicted, its buffers kept as a spare

@@ -665,7 +665,10 @@ int ensure_init() {
 // verify workspace (stl::verify_ws_bytes: ~0.44 GB, ~0.7 GB with key dedup),
 // so a caller cycling through many streams must not grow device memory
 // without bound.  STL_MAX_STREAM_WORKSPACES overrides (1..64) at stl_init.
-constexpr int kDefaultCallerStreams = 4;
+// Default 8: stellard's JobQueue auto-tunes to min(CPUs, 4) + 2 = up to 6
+// workers (JobQueue.cpp:217-243), so one stream per worker stays resident
+// with room to spare -- 8 contexts hold <= 5.6 GB of the 288 GB.
+constexpr int kDefaultCallerStreams = 8;
 std::atomic<int> g_max_caller_streams{kDefaultCallerStreams};
 std::atomic<int>& max_caller_streams() { return g_max_caller_streams; }
 
