@@ -301,9 +301,11 @@ def config1_leg(V, torch, dev, stream, threads_share):
         return V.signed_blob_verify_batch_device(d_buf, d_off, d_len, out_words=words, out_status=status,
                                                  stream=stream)
 
-    def med(fn, reps=15, warm=3):
-        # warm calls: the device sat idle while the host legs ran, and the
-        # first calls of a stream also settle its automatic-dedup verdict
+    def med(fn, reps=21, warm=10):
+        # warm calls: the device sat idle while the host legs ran and its clock
+        # ramps back over the first ~10 calls of a millisecond each (measured:
+        # 1.23 -> 1.11 ms), and the first calls of a stream also settle its
+        # automatic-dedup verdict
         for _ in range(warm):
             fn()
         torch.cuda.synchronize()
